@@ -1,0 +1,175 @@
+/*
+ * quorum_intersection.h -- C-ABI of the MI355X-native quorum-intersection checker.
+ *
+ * The reference (fixxxedpoint/quorum_intersection, quorum_intersection.cpp) is a single
+ * C++14 executable with no library or FFI surface.  Its only contract is the process
+ * interface (stellarbeat JSON on stdin, -h/-v/-g/-t/-p/-i/-m/-c, "true"/"false" and
+ * exit 0/1, cpp:744-800), which the `quorum_intersection` binary built from this library
+ * reproduces.  This header is the seam beneath it: plain pointers and sizes, no C++ or
+ * torch types, int status codes (0 = OK) and a thread-local error string.  Each entry
+ * point names the reference code it replaces.
+ *
+ * Threading: one host thread per qi_fbas / qi_search (the reference's findBestNode RNG
+ * and search counter are process-global statics, cpp:207/258).
+ */
+#ifndef QUORUM_INTERSECTION_H_
+#define QUORUM_INTERSECTION_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QI_ABI_VERSION 1
+
+enum {
+  QI_OK = 0,
+  QI_ERR_PARSE = 1,       /* JSON / schema error: the reference throws ptree_error and aborts */
+  QI_ERR_DEVICE = 2,      /* HIP runtime error, or no GPU: the product never falls back to CPU */
+  QI_ERR_ARG = 3,
+  QI_ERR_UNSUPPORTED = 4, /* searched SCC beyond the compiled kernel shapes (|SCC| > 256) */
+  QI_ERR_CAPACITY = 5,
+  QI_ERR_STATE = 6
+};
+
+/* findBestNode tie-break (cpp:203-250).  The reference samples uniformly among the
+ * maximal in-degree vertices; QI_TIE_LOWEST picks the lowest vertex index of that set,
+ * which is one of the reference's possible executions and makes counts reproducible. */
+enum { QI_TIE_LOWEST = 0 };
+
+typedef struct qi_fbas qi_fbas;
+typedef struct qi_search qi_search;
+
+const char* qi_last_error(void);
+int qi_abi_version(void);
+/* Number of visible HIP devices (0 when none). */
+int qi_device_count(void);
+
+/* ---------------------------------------------------------------------------------
+ * FBAS: parseStellarConfigurationJSON + buildDependencyGraph + strong_components
+ * (cpp:402-473, 615-633), host side.  `device` is the HIP ordinal used by the device
+ * entry points below (checked lazily, at the first device call).
+ * ------------------------------------------------------------------------------- */
+int qi_fbas_from_json(const char* json, size_t len, int device, qi_fbas** out);
+void qi_fbas_destroy(qi_fbas* f);
+uint32_t qi_fbas_num_vertices(const qi_fbas* f);
+uint32_t qi_fbas_num_edges(const qi_fbas* f);
+uint32_t qi_fbas_num_sccs(const qi_fbas* f);
+/* comp[v] = boost::strong_components id of vertex v (cpp:621); n entries. */
+int qi_fbas_scc_ids(const qi_fbas* f, uint32_t* comp);
+/* Adjacency in insertion order (cpp:458): offsets[n+1], targets[num_edges]. */
+int qi_fbas_adjacency(const qi_fbas* f, uint32_t* offsets, uint32_t* targets);
+/* Vertex strings (publicKey, name); pointers valid while f lives. */
+int qi_fbas_vertex(const qi_fbas* f, uint32_t v, const char** public_key, const char** name);
+
+/* ---------------------------------------------------------------------------------
+ * containsQuorum (cpp:140-177), batched on the GPU: for query b, the greatest fixpoint
+ * of f(X) = {x in X : x has a quorum slice in X ∪ F} starting from X = nodes_b ∩ avail_b
+ * with F = avail_b \ nodes_b always available.  Masks are ceil(n/64) uint64 words per
+ * query (bit v%64 of word v/64 = vertex v), host memory.  out_b = surviving vertices
+ * (the reference returns them in the order of `nodes`; as a set this is the same).
+ * ------------------------------------------------------------------------------- */
+int qi_gfp_batch(qi_fbas* f, const uint64_t* nodes, const uint64_t* avail, uint32_t count, uint64_t* out);
+
+/* ---------------------------------------------------------------------------------
+ * solve(Graph) (cpp:615-707): per-SCC quorum checks (cpp:649-672, batched on the GPU),
+ * the "exactly one SCC contains a quorum" rule (cpp:681-688) and the branch-and-bound
+ * search on sccs.front() (checkMinimalQuorums, cpp:348-400 / 691) on the GPU.
+ * ------------------------------------------------------------------------------- */
+typedef struct {
+  uint32_t tiebreak;       /* QI_TIE_LOWEST */
+  uint32_t grow_budget;    /* 0 = default: per-lane node budget while the frontier grows */
+  uint32_t run_budget;     /* 0 = default: per-lane node budget at full occupancy */
+  uint32_t max_blocks;     /* 0 = default (8 wavefronts per CU) */
+} qi_solve_opts;
+
+typedef struct {
+  int32_t verdict;         /* 1 = all quorums intersect ("true"), 0 = "false" */
+  int32_t searched;        /* 1 if checkMinimalQuorums ran */
+  uint32_t n_vertices;
+  uint32_t n_sccs;
+  uint32_t sccs_with_quorum;
+  uint32_t front_size;     /* |sccs.front()| */
+  uint64_t nodes;          /* iterateMinimalQuorums calls, preorder-exact (cpp:258) */
+  uint64_t evals;          /* containsQuorum calls the reference makes, all call sites */
+  uint64_t scc_evals;      /* of which per-SCC checks (cpp:658) */
+  uint64_t minq;           /* minimal quorums visited (cpp:361) */
+  uint64_t zero_fallback;  /* findBestNode default *quorum.begin() taken (cpp:221) */
+  uint64_t rounds;         /* Jacobi fixpoint rounds executed on the device (work metric) */
+  uint64_t launches;       /* search kernel launches */
+  uint32_t q1_len, q2_len; /* witness sizes (verdict 0 after a search) */
+  double t_scc_ms;         /* per-SCC checks, host wall */
+  double t_search_ms;      /* search, host wall */
+  double t_kernel_ms;      /* search kernels, HIP events */
+  uint32_t nonmonotone;    /* 1 if the searched SCC has threshold-0 quorum sets: the
+                              reference's fixpoints then depend on its sweep order, which
+                              at cpp:301 is libstdc++ unordered_set iteration order; the
+                              device search uses Jacobi rounds there (parity unpinned) */
+  uint32_t reserved;
+} qi_solve_result;
+
+/* q1, q2: caller buffers of n_vertices entries (may be NULL).  q1 = disjoint quorum
+ * found by the visitor, in sccs.front() order; q2 = the minimal quorum, in branch order
+ * (cpp:372-373).  Global vertex indices. */
+int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32_t* q1, uint32_t* q2);
+
+/* Text-mode driver = the reference's solve(istream&, ostream&, verbose, graphviz)
+ * (cpp:709-716) + verdict line (cpp:790-797).  Returns malloc'd text (free with
+ * qi_free); *verdict = 1/0.  verbose/graphviz as -v/-g. */
+int qi_solve_text(qi_fbas* f, int verbose, int graphviz, char** text, int* verdict);
+/* computePageRank (cpp:718-733) text ("PageRank:" + "label: value" lines), host float. */
+int qi_pagerank_text(qi_fbas* f, float dangling, float convergence, uint64_t max_iterations, char** text);
+void qi_free(void* p);
+
+/* ---------------------------------------------------------------------------------
+ * Step-wise search for multi-process drivers (one process per GPU, RCCL over xGMI in
+ * the caller).  A unit is a subtree root of iterateMinimalQuorums (cpp:252) packed in
+ * qi_search_unit_bytes() bytes; units can be moved between ranks through caller-owned
+ * device memory.  Counts stay preorder-exact because every processed segment is logged
+ * with its root path key and reduced against the globally preorder-first witness.
+ * ------------------------------------------------------------------------------- */
+typedef struct {
+  uint32_t grow_budget, run_budget, max_blocks; /* 0 = defaults */
+} qi_search_opts;
+
+typedef struct {
+  uint64_t frontier_in, frontier_out, processed;
+  uint32_t budget, blocks;
+  uint64_t new_witnesses;
+  double kernel_ms;
+} qi_step_info;
+
+typedef struct {
+  uint64_t nodes, evals, minq, zero_fallback, rounds;
+} qi_totals;
+
+/* Requires exactly one SCC with a quorum (else QI_ERR_STATE: no search is defined). */
+int qi_search_create(qi_fbas* f, const qi_search_opts* opts, qi_search** out);
+void qi_search_destroy(qi_search* s);
+uint32_t qi_search_unit_bytes(const qi_search* s);
+uint32_t qi_search_key_words(const qi_search* s);  /* 32-bit words of a path key */
+int qi_search_reset(qi_search* s);                  /* frontier = {root} (cpp:393) */
+int qi_search_clear(qi_search* s);                  /* frontier = {} */
+int qi_search_step(qi_search* s, qi_step_info* info);
+uint64_t qi_search_frontier(const qi_search* s);
+int qi_search_keep_slice(qi_search* s, uint64_t begin, uint64_t end);
+int qi_search_export(qi_search* s, uint64_t count, void* device_dst); /* pop `count` from the tail */
+int qi_search_import(qi_search* s, uint64_t count, const void* device_src);
+/* Best witness found locally: key[key_words], depth; returns 1 if any. */
+int qi_search_local_best(qi_search* s, uint32_t* key, uint32_t* depth);
+int qi_search_set_best(qi_search* s, const uint32_t* key, uint32_t depth);
+/* Sums over processed segments at or before (key, depth) in preorder; key NULL = all. */
+int qi_search_reduce(qi_search* s, const uint32_t* key, uint32_t depth, qi_totals* out);
+/* Witness of the local best: q1 (scc order) / q2 (branch order), global indices. */
+int qi_search_witness(qi_search* s, uint32_t* q1, uint32_t* q1_len, uint32_t* q2, uint32_t* q2_len);
+/* Forget processed segments / best (start a fresh search on the same FBAS). */
+int qi_search_restart(qi_search* s);
+double qi_search_kernel_ms(const qi_search* s);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QUORUM_INTERSECTION_H_ */

@@ -1,0 +1,140 @@
+"""ctypes binding of the C-ABI in include/quorum_intersection.h.
+
+The shared library is built in-tree (quorum_intersection_amd/_lib/libqi_amd.so) by
+``__graft_entry__.build()``; importing this module without it raises immediately --
+there is no CPU fallback for the hot path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_size_t, c_uint32, c_uint64, c_void_p
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libqi_amd.so")
+
+QI_OK = 0
+QI_ERR_PARSE = 1
+QI_ERR_DEVICE = 2
+QI_ERR_ARG = 3
+QI_ERR_UNSUPPORTED = 4
+QI_ERR_CAPACITY = 5
+QI_ERR_STATE = 6
+
+
+class QIError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[qi error {code}] {msg}")
+        self.code = code
+
+
+class SolveOpts(ctypes.Structure):
+    _fields_ = [("tiebreak", c_uint32), ("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32)]
+
+
+class SolveResult(ctypes.Structure):
+    _fields_ = [
+        ("verdict", c_int32),
+        ("searched", c_int32),
+        ("n_vertices", c_uint32),
+        ("n_sccs", c_uint32),
+        ("sccs_with_quorum", c_uint32),
+        ("front_size", c_uint32),
+        ("nodes", c_uint64),
+        ("evals", c_uint64),
+        ("scc_evals", c_uint64),
+        ("minq", c_uint64),
+        ("zero_fallback", c_uint64),
+        ("rounds", c_uint64),
+        ("launches", c_uint64),
+        ("q1_len", c_uint32),
+        ("q2_len", c_uint32),
+        ("t_scc_ms", c_double),
+        ("t_search_ms", c_double),
+        ("t_kernel_ms", c_double),
+        ("nonmonotone", c_uint32),
+        ("reserved", c_uint32),
+    ]
+
+
+class SearchOpts(ctypes.Structure):
+    _fields_ = [("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32)]
+
+
+class StepInfo(ctypes.Structure):
+    _fields_ = [
+        ("frontier_in", c_uint64),
+        ("frontier_out", c_uint64),
+        ("processed", c_uint64),
+        ("budget", c_uint32),
+        ("blocks", c_uint32),
+        ("new_witnesses", c_uint64),
+        ("kernel_ms", c_double),
+    ]
+
+
+class Totals(ctypes.Structure):
+    _fields_ = [("nodes", c_uint64), ("evals", c_uint64), ("minq", c_uint64), ("zero_fallback", c_uint64),
+                ("rounds", c_uint64)]
+
+
+# name -> (restype, argtypes); must match include/quorum_intersection.h exactly
+SIGNATURES = {
+    "qi_last_error": (c_char_p, []),
+    "qi_abi_version": (c_int, []),
+    "qi_device_count": (c_int, []),
+    "qi_fbas_from_json": (c_int, [c_char_p, c_size_t, c_int, POINTER(c_void_p)]),
+    "qi_fbas_destroy": (None, [c_void_p]),
+    "qi_fbas_num_vertices": (c_uint32, [c_void_p]),
+    "qi_fbas_num_edges": (c_uint32, [c_void_p]),
+    "qi_fbas_num_sccs": (c_uint32, [c_void_p]),
+    "qi_fbas_scc_ids": (c_int, [c_void_p, POINTER(c_uint32)]),
+    "qi_fbas_adjacency": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+    "qi_fbas_vertex": (c_int, [c_void_p, c_uint32, POINTER(c_char_p), POINTER(c_char_p)]),
+    "qi_gfp_batch": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_uint32, POINTER(c_uint64)]),
+    "qi_solve": (c_int, [c_void_p, POINTER(SolveOpts), POINTER(SolveResult), POINTER(c_uint32), POINTER(c_uint32)]),
+    "qi_solve_text": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int)]),
+    "qi_pagerank_text": (c_int, [c_void_p, c_float, c_float, c_uint64, POINTER(c_void_p)]),
+    "qi_free": (None, [c_void_p]),
+    "qi_search_create": (c_int, [c_void_p, POINTER(SearchOpts), POINTER(c_void_p)]),
+    "qi_search_destroy": (None, [c_void_p]),
+    "qi_search_unit_bytes": (c_uint32, [c_void_p]),
+    "qi_search_key_words": (c_uint32, [c_void_p]),
+    "qi_search_reset": (c_int, [c_void_p]),
+    "qi_search_clear": (c_int, [c_void_p]),
+    "qi_search_step": (c_int, [c_void_p, POINTER(StepInfo)]),
+    "qi_search_frontier": (c_uint64, [c_void_p]),
+    "qi_search_keep_slice": (c_int, [c_void_p, c_uint64, c_uint64]),
+    "qi_search_export": (c_int, [c_void_p, c_uint64, c_void_p]),
+    "qi_search_import": (c_int, [c_void_p, c_uint64, c_void_p]),
+    "qi_search_local_best": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+    "qi_search_set_best": (c_int, [c_void_p, POINTER(c_uint32), c_uint32]),
+    "qi_search_reduce": (c_int, [c_void_p, POINTER(c_uint32), c_uint32, POINTER(Totals)]),
+    "qi_search_witness": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32),
+                                  POINTER(c_uint32)]),
+    "qi_search_restart": (c_int, [c_void_p]),
+    "qi_search_kernel_ms": (c_double, [c_void_p]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the in-tree HIP library; raise if it is missing (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950) first")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.qi_abi_version() != 1:
+            raise ImportError("libqi_amd.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != QI_OK:
+        raise QIError(rc, lib().qi_last_error().decode(errors="replace"))

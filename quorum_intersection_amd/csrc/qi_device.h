@@ -1,0 +1,89 @@
+// Internal interface between the host driver and the HIP device code (qi_device.hip).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "qi_internal.h"
+
+namespace qi {
+
+// ----------------------------------------------------------------------------------
+// Batched greatest-fixpoint evaluation (containsQuorum, cpp:140-177) over the global
+// threshold-node CSR: one wavefront per query, membership by wave64 __ballot.
+// ----------------------------------------------------------------------------------
+class GfpDevice {
+ public:
+  virtual ~GfpDevice() = default;
+  // nodes/avail/out: count x words(n) uint64 masks in host memory.
+  virtual void run(const uint64_t* nodes, const uint64_t* avail, uint32_t count, uint64_t* out) = 0;
+  virtual double last_kernel_ms() const = 0;
+};
+std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g);
+
+// ----------------------------------------------------------------------------------
+// Branch-and-bound search (iterateMinimalQuorums + checkMinimalQuorums, cpp:252-400)
+// as a budgeted frontier loop.  A "unit" is a subtree root (T, D, path key, D order);
+// one launch runs a per-lane depth-first walk of units for at most `budget` search
+// nodes per lane, spilling the rest of its stack back into the next frontier.
+// ----------------------------------------------------------------------------------
+struct SearchConfig {
+  uint32_t max_blocks = 0;       // 0 = CUs * 8
+  uint32_t grow_budget = 48;     // per-lane node budget while the frontier is small
+  uint32_t run_budget = 4096;    // per-lane node budget once the frontier fills the GPU
+  uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output)
+  bool keep_log = true;          // keep per-segment records for preorder-exact counts
+};
+
+struct StepInfo {
+  uint64_t frontier_in = 0, frontier_out = 0;
+  uint64_t processed = 0;        // units fetched this launch
+  uint32_t budget = 0, blocks = 0;
+  uint64_t new_witnesses = 0;
+  double kernel_ms = 0;          // HIP-event time of the search kernel
+  bool has_best = false;
+};
+
+struct Totals {
+  uint64_t nodes = 0, evals = 0, minq = 0, zero_fallback = 0, rounds = 0;
+};
+
+struct Witness {
+  std::vector<uint32_t> key;     // path bits, MSB-first words
+  uint32_t depth = 0;
+  std::vector<uint32_t> q1_local;  // ascending local indices (visitor GFP survivors)
+  std::vector<uint32_t> q2_local;  // D in branch order
+};
+
+class SearchDevice {
+ public:
+  virtual ~SearchDevice() = default;
+  virtual uint32_t key_words() const = 0;
+  virtual uint32_t unit_bytes() const = 0;
+  virtual void reset_root() = 0;                    // frontier = {root of cpp:393}
+  virtual void clear_frontier() = 0;
+  virtual StepInfo step() = 0;                      // one launch + compaction
+  virtual uint64_t frontier_size() const = 0;
+  // Frontier hand-off for multi-rank rebalancing: units are moved through caller-owned
+  // device memory (e.g. torch tensors sent with RCCL).
+  virtual void export_tail(uint64_t count, void* dev_dst) = 0;
+  virtual void import_units(uint64_t count, const void* dev_src) = 0;
+  virtual void keep_slice(uint64_t begin, uint64_t end) = 0;
+  // Global best (preorder-first witness key) known to the caller, for pruning.
+  virtual void set_best(const std::vector<uint32_t>& key, uint32_t depth) = 0;
+  virtual bool best(Witness* w) const = 0;          // best witness found on this device
+  // Sums over every processed segment whose root precedes-or-equals `key` in preorder
+  // (all segments when has_key == false).
+  virtual Totals reduce(bool has_key, const std::vector<uint32_t>& key, uint32_t depth) = 0;
+  virtual Totals running_totals() const = 0;        // unfiltered running sums
+  virtual void drop_log() = 0;                      // forget processed segments
+  virtual double sum_kernel_ms() const = 0;
+  virtual uint64_t launches() const = 0;
+};
+std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg);
+
+int device_count();
+int device_cu_count(int device);
+
+}  // namespace qi

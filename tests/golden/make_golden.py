@@ -1,0 +1,51 @@
+"""Regenerate tests/golden/golden.json from the CPU oracle (oracle/qi_oracle.cpp).
+
+The only reference-held known answers are the four fixture verdicts (correct*.json ->
+true, broken*.json -> false; /root/reference/README.md:25-28).  Everything else here
+(search-node counts, fixpoint-eval counts, minimal quorums visited, witnesses, SCC
+facts) is produced by the oracle under the deterministic "lowest index" tie-break of
+findBestNode (cpp:203-250) and pinned so later rounds cannot drift.
+
+    python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from qi_testlib import FIXTURES, Oracle, fixture_text, random_fbas  # noqa: E402
+from quorum_intersection_amd import fbas_gen  # noqa: E402
+
+KEYS = ["verdict", "n", "nscc", "scc_with_quorum", "scc_quorum_ids", "front", "searched", "nodes", "evals",
+        "scc_evals", "minq", "zero_fallback", "q1", "q2"]
+
+
+def instances():
+    for name in FIXTURES:
+        yield name, fixture_text(name).decode()
+    for k in range(2, 8):
+        yield f"tiered_{k}", fbas_gen.tiered(k)
+    yield "two_tier_7_256", fbas_gen.two_tier(7, 256)
+    yield "tiered_5_shuffled", fbas_gen.tiered(5, seed=3)
+    for k, n in ((4, 64), (5, 96)):
+        yield f"planted_{k}_{n}", fbas_gen.planted(k, n)
+    for s in range(40):
+        yield f"random_{s}", random_fbas(s)
+
+
+def main():
+    o = Oracle()
+    out = {}
+    for name, text in instances():
+        r = o.load(text).solve()
+        out[name] = {k: r[k] for k in KEYS}
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print(f"wrote {len(out)} instances")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,290 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle / golden vectors.
+
+Bar: bit-exact verdicts, preorder-exact search-node counts, exact credited fixpoint-eval
+counts, minimal quorums visited and witnesses, under the deterministic lowest-index
+tie-break (a possible execution of the reference's random one);
+bit-exact containsQuorum survivor sets.  Every test here runs HIP kernels on cuda:0.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from qi_testlib import FIXTURES, GOLDEN, ROOT, Oracle, fixture_text, random_fbas, random_masks, random_org_fbas
+import quorum_intersection_amd as qa
+from quorum_intersection_amd import fbas_gen
+
+pytestmark = pytest.mark.gpu
+GOLD = json.load(open(os.path.join(GOLDEN, "golden.json")))
+CMP = ["verdict", "nodes", "evals", "scc_evals", "minq", "zero_fallback", "q1", "q2"]
+
+
+def _cmp(d, r, name):
+    if d.get("nonmonotone"):
+        pytest.skip(f"{name}: threshold-0 sets in the searched SCC (search parity unpinned)")
+    assert d["verdict"] == r["verdict"], name
+    assert d["nodes"] == r["nodes"], (name, d["nodes"], r["nodes"])
+    assert d["evals"] == r["evals"], (name, d["evals"], r["evals"])
+    assert d["scc_evals"] == r["scc_evals"], name
+    assert d["minq"] == r["minq"], name
+    assert d["zero_fallback"] == r["zero_fallback"], name
+    assert d["q1"] == r["q1"] and d["q2"] == r["q2"], (name, d["q1"], d["q2"], r["q1"], r["q2"])
+    assert d["sccs_with_quorum"] == r["scc_with_quorum"]
+    assert d["n_sccs"] == r["nscc"]
+    assert d["searched"] == r["searched"]
+
+
+def _text_for(name):
+    if name in FIXTURES:
+        return fixture_text(name)
+    if name == "tiered_5_shuffled":
+        return fbas_gen.tiered(5, seed=3)
+    if name.startswith("tiered_"):
+        return fbas_gen.tiered(int(name.split("_")[1]))
+    if name.startswith("two_tier_"):
+        _, _, k, n = name.split("_")
+        return fbas_gen.two_tier(int(k), int(n))
+    if name.startswith("planted_"):
+        _, k, n = name.split("_")
+        return fbas_gen.planted(int(k), int(n))
+    return random_fbas(int(name.split("_")[1]))
+
+
+def _validate_witness(text, q1, q2):
+    """Independent witness check with the oracle's slice predicate: Q1 ∩ Q2 = ∅, both in
+    the main SCC, every v in Q2 has a slice inside Q2 (outside unavailable), every v in
+    Q1 has a slice inside Q1 ∪ (V \\ scc) (outside available, cpp:354/368)."""
+    g = Oracle().load(text)
+    r = g.solve()
+    scc = set(r["front"])
+    assert q1 and q2 and not (set(q1) & set(q2))
+    assert set(q1) <= scc and set(q2) <= scc
+    a2 = [v in set(q2) for v in range(g.n)]
+    assert all(g.slice(v, a2) for v in q2)
+    a1 = [(v in set(q1)) or (v not in scc) for v in range(g.n)]
+    assert all(g.slice(v, a1) for v in q1)
+
+
+# ---- containsQuorum ------------------------------------------------------------------
+@pytest.mark.parametrize("name", FIXTURES)
+def test_gfp_batch_fixtures(name):
+    text = fixture_text(name)
+    f, g = qa.FBAS(text), Oracle().load(text)
+    rng = random.Random(7)
+    nodes = random_masks(rng, f.n, 200, 0.7) + [list(range(f.n))] + f.sccs()
+    avail = [sorted(set(s) | {v for v in range(f.n) if rng.random() < 0.3}) for s in nodes]
+    out = qa.sets_from_masks(f.gfp_batch(qa.masks_from_sets(nodes, f.n), qa.masks_from_sets(avail, f.n)), f.n)
+    for s, a, o in zip(nodes, avail, out):
+        av = [v in set(a) for v in range(f.n)]
+        assert sorted(g.contains_quorum(s, av)) == o
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_gfp_batch_random(seed):
+    # threshold-0 sets included: the batched kernel runs exact ascending Gauss-Seidel then
+    text = random_fbas(seed, n=30) if seed % 2 else random_org_fbas(seed, 8, t0=True)
+    f, g = qa.FBAS(text), Oracle().load(text)
+    rng = random.Random(seed)
+    nodes = random_masks(rng, f.n, 64, rng.uniform(0.3, 0.95))
+    avail = [sorted(set(s) | {v for v in range(f.n) if rng.random() < 0.2}) for s in nodes]
+    out = qa.sets_from_masks(f.gfp_batch(qa.masks_from_sets(nodes, f.n), qa.masks_from_sets(avail, f.n)), f.n)
+    for s, a, o in zip(nodes, avail, out):
+        av = [v in set(a) for v in range(f.n)]
+        assert sorted(g.contains_quorum(s, av)) == o
+
+
+def test_contains_quorum_api_order():
+    text = fixture_text("correct")
+    f, g = qa.FBAS(text), Oracle().load(text)
+    nodes = list(range(f.n))[::-1]
+    av = [True] * f.n
+    assert f.containsQuorum(nodes, av) == g.contains_quorum(nodes, av)
+
+
+# ---- solve(Graph): verdict, counts, witness --------------------------------------------
+@pytest.mark.parametrize("name", sorted(GOLD))
+def test_solve_matches_golden(name):
+    text = _text_for(name)
+    d = qa.FBAS(text).solve_stats()
+    _cmp(d, GOLD[name], name)
+    if not d["verdict"] and d["searched"]:
+        _validate_witness(text, d["q1"], d["q2"])
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_solve_random_org(seed):
+    text = random_org_fbas(seed, n_orgs=5 + seed % 4)
+    r = Oracle().load(text).solve()
+    d = qa.FBAS(text).solve_stats()
+    _cmp(d, r, f"org{seed}")
+    if not d["verdict"] and d["searched"]:
+        _validate_witness(text, d["q1"], d["q2"])
+
+
+@pytest.mark.parametrize("cfg", [(1, 1, 1), (2, 3, 1), (3, 5, 2), (1, 7, 4), (5, 64, 3)])
+def test_solve_tiny_budgets_exercise_the_frontier(cfg):
+    # budgets of a few nodes per lane force many launches, spills, ring carry-overs and
+    # (with one block) LDS-stack evictions; counts must not change
+    grow, run, blocks = cfg
+    for name in ("tiered_4", "tiered_5", "broken", "correct", "planted_4_64", "tiered_5_shuffled"):
+        d = qa.FBAS(_text_for(name)).solve_stats(grow, run, blocks)
+        _cmp(d, GOLD[name], name)
+    for seed in (0, 4, 9, 12, 16, 17):
+        text = random_org_fbas(seed, n_orgs=5 + seed % 4)
+        _cmp(qa.FBAS(text).solve_stats(grow, run, blocks), Oracle().load(text).solve(), f"org{seed}")
+
+
+def test_solve_tiered_6_7_exact():
+    for k in (6, 7):
+        d = qa.FBAS(fbas_gen.tiered(k)).solve_stats()
+        _cmp(d, GOLD[f"tiered_{k}"], k)
+
+
+def test_solve_two_tier_256():
+    d = qa.FBAS(fbas_gen.two_tier(7, 256)).solve_stats()
+    _cmp(d, GOLD["two_tier_7_256"], "two_tier_7_256")
+
+
+def test_tiered_8_full_search_counts():
+    # 1,857,737 search calls, 3,030,461 fixpoint evals, 20,412 minimal quorums
+    d = qa.FBAS(fbas_gen.tiered(8)).solve_stats()
+    assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (True, 1857737, 3030461 + 0, 20412)
+
+
+def test_large_scc_multiword_masks():
+    # |SCC| in (32, 64] and (64, 128]: 2- and 4-word masks (planted witnesses keep the
+    # oracle's search short)
+    for k, n in ((11, 60), (20, 80), (28, 120)):
+        text = fbas_gen.planted(k, n)
+        r = Oracle().load(text).solve()
+        assert len(r["front"]) > 32
+        d = qa.FBAS(text).solve_stats()
+        _cmp(d, r, f"planted_{k}_{n}")
+        if not d["verdict"]:
+            _validate_witness(text, d["q1"], d["q2"])
+
+
+def test_multiword_random_exact():
+    for seed in range(8):
+        text = random_org_fbas(1000 + seed, n_orgs=14)
+        r = Oracle().load(text).solve(budget=600_000)
+        if r["aborted"]:
+            continue
+        _cmp(qa.FBAS(text).solve_stats(), r, f"big{seed}")
+
+
+# ---- text outputs (-v / -g) ------------------------------------------------------------
+@pytest.mark.parametrize("name", FIXTURES)
+def test_solve_text_matches_oracle(name):
+    text = fixture_text(name)
+    g = Oracle().load(text)
+    for v, gv in ((False, False), (True, False), (False, True), (True, True)):
+        out, verdict = qa.FBAS(text).solve_text(v, gv)
+        assert out == g.solve_text(v, gv)
+        assert verdict == name.startswith("correct")
+
+
+def test_cli_binary_verdicts_and_exit_codes():
+    import subprocess
+    exe = os.path.join(ROOT, "bin", "quorum_intersection")
+    for name in FIXTURES:
+        r = subprocess.run([exe], input=fixture_text(name), capture_output=True)
+        ok = name.startswith("correct")
+        assert r.stdout == (b"true\n" if ok else b"false\n")
+        assert r.returncode == (0 if ok else 1)
+        r = subprocess.run([exe, "-v"], input=fixture_text(name), capture_output=True)
+        assert r.stdout.decode() == Oracle().load(fixture_text(name)).solve_text(True, False)
+
+
+# ---- step-wise search with frontier hand-off (the multi-rank protocol on one GPU) -------
+def _two_way_search(text, hand_every=1, move_frac=0.5):
+    import ctypes
+    import torch
+    from quorum_intersection_amd import _capi
+    L = _capi.lib()
+    fa, fb = qa.FBAS(text), qa.FBAS(text)
+    sa, sb = ctypes.c_void_p(), ctypes.c_void_p()
+    opts = _capi.SearchOpts(2, 8, 2)
+    _capi.check(L.qi_search_create(fa.handle, ctypes.byref(opts), ctypes.byref(sa)))
+    _capi.check(L.qi_search_create(fb.handle, ctypes.byref(opts), ctypes.byref(sb)))
+    _capi.check(L.qi_search_clear(sb))
+    ub = L.qi_search_unit_bytes(sa)
+    kw = L.qi_search_key_words(sa)
+    it = 0
+    while L.qi_search_frontier(sa) + L.qi_search_frontier(sb):
+        for s in (sa, sb):
+            if L.qi_search_frontier(s):
+                _capi.check(L.qi_search_step(s, None))
+        it += 1
+        if it % hand_every == 0:  # move part of the larger frontier to the other side
+            na, nb = L.qi_search_frontier(sa), L.qi_search_frontier(sb)
+            src, dst, cnt = (sa, sb, na) if na > nb else (sb, sa, nb)
+            mv = int((cnt - min(na, nb)) * move_frac)
+            if mv:
+                buf = torch.empty(mv * ub, dtype=torch.uint8, device="cuda")
+                _capi.check(L.qi_search_export(src, mv, ctypes.c_void_p(buf.data_ptr())))
+                _capi.check(L.qi_search_import(dst, mv, ctypes.c_void_p(buf.data_ptr())))
+        # exchange best keys both ways (what the RCCL all-reduce does across ranks)
+        keys = []
+        for s in (sa, sb):
+            k = (ctypes.c_uint32 * kw)()
+            d = ctypes.c_uint32()
+            if L.qi_search_local_best(s, k, ctypes.byref(d)) == 1:
+                keys.append((list(k), d.value))
+        if keys:
+            k, d = min(keys)
+            for s in (sa, sb):
+                _capi.check(L.qi_search_set_best(s, (ctypes.c_uint32 * kw)(*k), d))
+    keys = []
+    for s in (sa, sb):
+        k = (ctypes.c_uint32 * kw)()
+        d = ctypes.c_uint32()
+        if L.qi_search_local_best(s, k, ctypes.byref(d)) == 1:
+            keys.append((list(k), d.value, s))
+    tot = [0, 0, 0]
+    best = min(keys) if keys else None
+    for s in (sa, sb):
+        t = _capi.Totals()
+        if best:
+            _capi.check(L.qi_search_reduce(s, (ctypes.c_uint32 * kw)(*best[0]), best[1], ctypes.byref(t)))
+        else:
+            _capi.check(L.qi_search_reduce(s, None, 0, ctypes.byref(t)))
+        tot[0] += t.nodes
+        tot[1] += t.evals
+        tot[2] += t.minq
+    res = {"verdict": best is None, "nodes": tot[0], "evals": tot[1], "minq": tot[2]}
+    if best:
+        q1 = (ctypes.c_uint32 * fa.n)()
+        q2 = (ctypes.c_uint32 * fa.n)()
+        l1, l2 = ctypes.c_uint32(), ctypes.c_uint32()
+        _capi.check(L.qi_search_witness(best[2], q1, ctypes.byref(l1), q2, ctypes.byref(l2)))
+        res["q1"], res["q2"] = list(q1)[: l1.value], list(q2)[: l2.value]
+    L.qi_search_destroy(sa)
+    L.qi_search_destroy(sb)
+    return res
+
+
+@pytest.mark.parametrize("name", ["tiered_4", "tiered_5", "broken", "planted_5_96", "correct"])
+def test_two_way_frontier_handoff_exact(name):
+    text = _text_for(name)
+    r = GOLD[name]
+    d = _two_way_search(text)
+    assert d["verdict"] == r["verdict"]
+    assert d["nodes"] == r["nodes"]
+    assert d["evals"] == r["evals"] - r["scc_evals"]
+    assert d["minq"] == r["minq"]
+    if not r["verdict"]:
+        assert d["q1"] == r["q1"] and d["q2"] == r["q2"]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 7, 11, 12, 16])
+def test_two_way_handoff_random_witness(seed):
+    text = random_org_fbas(seed, n_orgs=5 + seed % 4)
+    r = Oracle().load(text).solve()
+    if not r["searched"]:
+        pytest.skip("no search")
+    d = _two_way_search(text, hand_every=1, move_frac=0.7)
+    assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"],
+                                                                 r["evals"] - r["scc_evals"], r["minq"])
