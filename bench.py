@@ -1,0 +1,231 @@
+#!/usr/bin/env python
+"""bench.py -- quorum-fixpoint evals/sec + time-to-verdict on a 256-validator tiered FBAS.
+
+Workload (BASELINE.json configs[3]): G2 two_tier(k_top, 256) -- a top tier
+of k_top organisations x 3 validators (inner 2-of-3, outer ceil(2k/3)-of-k) that is the
+searched SCC, plus 256 - 3k lower validators in organisations of 3.  k_top = 10 by
+default: the repo's single-threaded -O3 CPU restatement of the reference needs ~450 s for
+its full search (121,164,209 search nodes, 204,527,236 credited fixpoint evals), inside
+the survey's 60-600 s window.
+
+One "step" = one full solve of the resident FBAS: the per-SCC quorum checks (batched
+GFP kernel, cpp:649-672) plus the complete branch-and-bound search (cpp:348-400), i.e.
+time-to-verdict with inputs already in HBM.  value = credited fixpoint evaluations of
+all ranks / max-over-ranks time.  N>1: one process per GPU (torch.distributed, RCCL),
+the search tree sharded by branch prefix (quorum_intersection_amd.distributed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--k-top 10] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# MI355X (gfx950) int32 VALU peak: 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz; a wave64
+# VALU op issues in 2 cycles on a SIMD32 (MI355X_MICROARCH.md, chip table + "wave
+# scheduling"; the same rate gives its 157.3 TFLOP/s fp32 FMA peak).
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+
+
+def ops_per_round(sh):
+    """Algorithmic int32 lane-ops of one Jacobi round of containsQuorum on the flattened
+    SCC: per threshold node AND+BCNT per vertex word, AND+BCNT per child-sat word (nodes
+    with children), threshold compare + satisfaction bit; per distinct root a bit test +
+    OR of its users; per vertex word the AND with X and the stability compare."""
+    w = sh["mask_words"]
+    return (sh["tns"] * (2 * w + 2) + sh["tns_with_children"] * 2 + 2 * sh["extra_terms"]
+            + sh["roots"] * (w + 2) + 2 * w)
+
+
+def ops_per_best(sh):
+    """findBestNode on one internal node: per column group AND+BCNT of Q (degree), AND of
+    Q\\D with the members + find-first, and the compare/select."""
+    w = sh["mask_words"]
+    return sh["groups"] * (4 * w + 3)
+
+
+def cpu_baseline(text: str, sample_nodes: int) -> dict:
+    """The oracle (oracle/qi_oracle.cpp, -O3, one pinned core) on the first
+    `sample_nodes` search nodes of the same workload, in a child process."""
+    code = (
+        "import os, sys, json; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})\n"
+        "from qi_testlib import Oracle\n"
+        "t = sys.stdin.read()\n"
+        "r = Oracle().load(t).solve(budget=%d)\n"
+        "print(json.dumps(r))\n" % (ROOT, os.path.join(ROOT, "tests"), sample_nodes)
+    )
+    out = subprocess.run([sys.executable, "-c", code], input=text, capture_output=True, text=True, check=True)
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    return r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--k-top", type=int, default=10)
+    ap.add_argument("--validators", type=int, default=256)
+    ap.add_argument("--cpu-sample-nodes", type=int, default=4_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--grow-budget", type=int, default=0)
+    ap.add_argument("--run-budget", type=int, default=0)
+    ap.add_argument("--max-blocks", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import quorum_intersection_amd as qa
+    from quorum_intersection_amd import fbas_gen
+    from quorum_intersection_amd.distributed import DeviceSearch, distributed_search
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    text = fbas_gen.two_tier(args.k_top, args.validators)
+
+    # ---- time-to-verdict from JSON text (host parse + flatten + upload + solve), N=1 path
+    t0 = time.perf_counter()
+    fb = qa.FBAS(text, device=local)
+    ttv_res = fb.solve_stats(args.grow_budget, args.run_budget, args.max_blocks)
+    time_to_verdict = time.perf_counter() - t0
+
+    be = DeviceSearch(fb, args.grow_budget, args.run_budget, args.max_blocks)
+    shape = be.shape()
+    sccs = fb.sccs()
+    scc_masks = qa.masks_from_sets(sccs, fb.n)
+
+    def one_step():
+        fb.gfp_batch(scc_masks, scc_masks)          # per-SCC checks (cpp:649-672)
+        return distributed_search(be, device=dev)   # search (cpp:691 -> 348-400)
+
+    for _ in range(args.warmup):
+        one_step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    kernel_ms = 0.0
+    launches = 0
+    res = None
+    for _ in range(args.steps):
+        res = one_step()
+        kernel_ms += be.kernel_ms
+        launches += be.launches
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms, float(launches)], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        kernel_ms_all, launches_all = float(tsum[1]), int(tsum[2])
+    else:
+        kernel_ms_all, launches_all = kernel_ms, launches
+
+    evals_per_step = res.evals + len(sccs)   # + per-SCC checks (cpp:658), credited
+    value = evals_per_step * args.steps / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    # roofline of the dominant kernel (search_kernel): algorithmic int32 ops / kernel time
+    internal = (res.nodes - 1) // 2
+    alg_ops_step = res.rounds * ops_per_round(shape) + internal * ops_per_best(shape)
+    avg_launch_ms = kernel_ms_all / max(launches_all, 1)
+    alg_ops_launch = alg_ops_step * args.steps / max(launches_all, 1)
+    achieved = alg_ops_launch / (avg_launch_ms * 1e-3) / 1e12 if avg_launch_ms > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("k_top") == args.k_top and tj.get("validators") == args.validators:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    line = {
+        "metric": "quorum-fixpoint evals/sec + time-to-verdict, 256-validator tiered FBAS",
+        "value": value,
+        "unit": "fixpoint-evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (deterministic G2 generator, no random values)",
+        "config": {
+            "workload": f"two_tier(k_top={args.k_top}, n={args.validators}) full search, no early exit",
+            "validators": args.validators,
+            "searched_scc": shape["m"],
+            "search_nodes_per_step": res.nodes,
+            "evals_per_step": evals_per_step,
+            "verdict": res.verdict,
+            "parallelism": f"search-tree sharding x{world} (RCCL all_gather + send/recv)",
+        },
+        "roofline": {
+            "bound": "valu",
+            "achieved": achieved,
+            "peak": VALU_PEAK_TOPS,
+            "unit": "Tops/s (int32 lane-ops)",
+            "frac": achieved / VALU_PEAK_TOPS,
+            "traffic": traffic,
+            "kernel": "search_kernel",
+            "avg_launch_ms": avg_launch_ms,
+            "launches_per_step": launches_all / args.steps / world,
+        },
+        "time_to_verdict_s": time_to_verdict,
+        "time_to_verdict_note": "N=1 path from JSON text in host memory: parse, SCCs, flatten, upload, solve",
+    }
+    if ttv_res["nodes"] != res.nodes or ttv_res["evals"] != evals_per_step:
+        line["warning"] = "solve_stats and step-wise search disagree"
+
+    if not args.no_cpu_baseline and world == 1:
+        r = cpu_baseline(text, args.cpu_sample_nodes)
+        cpu_evals_s = r["evals"] / r["seconds"]
+        line["cpu_baseline"] = {
+            "value": cpu_evals_s,
+            "unit": "fixpoint-evals/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": (f"oracle/qi_oracle.cpp -O3, one pinned core: first {r['nodes']:,} search nodes "
+                       f"({r['evals']:,} evals incl. {r['scc_evals']} per-SCC checks) of the same workload "
+                       f"in {r['seconds']:.1f} s"),
+            "time_to_verdict_est_s": evals_per_step / cpu_evals_s,
+        }
+        line["speedup_vs_cpu"] = value / cpu_evals_s
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -145,6 +145,18 @@ typedef struct {
   uint64_t nodes, evals, minq, zero_fallback, rounds;
 } qi_totals;
 
+/* Shape of the flattened searched SCC (for work accounting). */
+typedef struct {
+  uint32_t m;          /* |sccs.front()| */
+  uint32_t mask_words; /* 32-bit words per vertex mask */
+  uint32_t tns;        /* live threshold nodes */
+  uint32_t tn_words;   /* 32-bit words per TN-satisfaction mask */
+  uint32_t tns_with_children;
+  uint32_t roots;      /* distinct root TNs */
+  uint32_t groups;     /* findBestNode column groups */
+  uint32_t extra_terms;
+} qi_shape;
+
 /* Requires exactly one SCC with a quorum (else QI_ERR_STATE: no search is defined). */
 int qi_search_create(qi_fbas* f, const qi_search_opts* opts, qi_search** out);
 void qi_search_destroy(qi_search* s);
@@ -167,6 +179,7 @@ int qi_search_witness(qi_search* s, uint32_t* q1, uint32_t* q1_len, uint32_t* q2
 /* Forget processed segments / best (start a fresh search on the same FBAS). */
 int qi_search_restart(qi_search* s);
 double qi_search_kernel_ms(const qi_search* s);
+int qi_search_shape(const qi_search* s, qi_shape* out);
 
 #ifdef __cplusplus
 }

@@ -72,6 +72,12 @@ class StepInfo(ctypes.Structure):
     ]
 
 
+class Shape(ctypes.Structure):
+    _fields_ = [("m", c_uint32), ("mask_words", c_uint32), ("tns", c_uint32), ("tn_words", c_uint32),
+                ("tns_with_children", c_uint32), ("roots", c_uint32), ("groups", c_uint32),
+                ("extra_terms", c_uint32)]
+
+
 class Totals(ctypes.Structure):
     _fields_ = [("nodes", c_uint64), ("evals", c_uint64), ("minq", c_uint64), ("zero_fallback", c_uint64),
                 ("rounds", c_uint64)]
@@ -113,6 +119,7 @@ SIGNATURES = {
                                   POINTER(c_uint32)]),
     "qi_search_restart": (c_int, [c_void_p]),
     "qi_search_kernel_ms": (c_double, [c_void_p]),
+    "qi_search_shape": (c_int, [c_void_p, POINTER(Shape)]),
 }
 
 _lib = None

@@ -428,4 +428,24 @@ int qi_search_restart(qi_search* s) {
 
 double qi_search_kernel_ms(const qi_search* s) { return s ? s->sd->sum_kernel_ms() : 0.0; }
 
+int qi_search_shape(const qi_search* s, qi_shape* out) {
+  if (!s || !out) return fail(QI_ERR_ARG, "null");
+  const qi::LocalFlat& L = s->lf;
+  out->m = L.m;
+  out->mask_words = L.mw;
+  out->tns = L.T;
+  out->tn_words = L.tw;
+  uint32_t wc = 0;
+  for (uint32_t t = 0; t < L.T; ++t) {
+    bool any = false;
+    for (uint32_t w = 0; w < L.tw; ++w) any |= L.cmask[(size_t)t * L.tw + w] != 0;
+    wc += any ? 1u : 0u;
+  }
+  out->tns_with_children = wc;
+  out->roots = L.R;
+  out->groups = L.G;
+  out->extra_terms = (uint32_t)L.extra_src.size();
+  return QI_OK;
+}
+
 }  // extern "C"

@@ -1,0 +1,311 @@
+"""Multi-GPU branch-and-bound search: one process per GPU, torch.distributed over RCCL.
+
+The search tree of iterateMinimalQuorums (quorum_intersection.cpp:252-346) is sharded
+by branch prefix: rank 0 starts from the root, and subtree units (branch prefixes) are
+handed to the other ranks as soon as its frontier grows; every rank then runs budgeted
+device launches on its own units.  Between launches the ranks exchange only
+
+  * frontier sizes + best-witness keys   (one all_gather of a few int64s), and
+  * surplus units for rebalancing         (send/recv of packed unit bytes, host-planned),
+
+so the data path has no collective.  Counts stay preorder-exact because every processed
+segment is logged with its root path key on the rank that processed it; at the end each
+rank reduces its log against the globally preorder-first witness and the totals are
+summed with one all_reduce.
+
+The coordination logic is backend-agnostic (``SearchBackend``): ``DeviceSearch`` wraps
+the C-ABI step-wise search on a HIP device; tests drive a synthetic CPU backend over the
+gloo process group.
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+Key = Tuple[Tuple[int, ...], int]  # (path key words, depth); preorder = lexicographic
+
+
+class SearchBackend:
+    """What the multi-rank driver needs from one rank's search engine."""
+
+    key_words: int
+    unit_bytes: int
+
+    def reset(self) -> None: ...
+    def clear(self) -> None: ...
+    def restart(self) -> None: ...
+    def drop_log(self) -> None: ...
+    def step(self) -> None: ...
+    def frontier(self) -> int: ...
+    def keep_slice(self, begin: int, end: int) -> None: ...
+    def export(self, count: int, dst: torch.Tensor) -> None: ...
+    def import_(self, count: int, src: torch.Tensor) -> None: ...
+    def local_best(self) -> Optional[Key]: ...
+    def set_best(self, key: Key) -> None: ...
+    def reduce(self, key: Optional[Key]) -> Dict[str, int]: ...
+    def witness(self) -> Tuple[List[int], List[int]]: ...
+
+
+class DeviceSearch(SearchBackend):
+    """C-ABI step-wise search (include/quorum_intersection.h) on one HIP device."""
+
+    def __init__(self, fbas, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0):
+        from . import _capi
+        self._c = _capi
+        self.L = _capi.lib()
+        self.fbas = fbas
+        h = ctypes.c_void_p()
+        opts = _capi.SearchOpts(grow_budget, run_budget, max_blocks)
+        _capi.check(self.L.qi_search_create(fbas.handle, ctypes.byref(opts), ctypes.byref(h)))
+        self.h = h
+        self.key_words = int(self.L.qi_search_key_words(h))
+        self.unit_bytes = int(self.L.qi_search_unit_bytes(h))
+        self.kernel_ms = 0.0
+        self.launches = 0
+
+    def close(self):
+        if self.h:
+            self.L.qi_search_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        self._c.check(self.L.qi_search_reset(self.h))
+
+    def clear(self):
+        self._c.check(self.L.qi_search_clear(self.h))
+
+    def restart(self):
+        self._c.check(self.L.qi_search_restart(self.h))
+        self.kernel_ms = 0.0
+        self.launches = 0
+
+    def drop_log(self):
+        # forget processed segments and bests but keep the current frontier
+        n = self.frontier()
+        keep = None
+        if n:
+            keep = torch.empty(n * self.unit_bytes, dtype=torch.uint8, device=f"cuda:{torch.cuda.current_device()}")
+            self.export(n, keep)
+        self._c.check(self.L.qi_search_restart(self.h))
+        self.clear()
+        if n:
+            self.import_(n, keep)
+
+    def step(self):
+        info = self._c.StepInfo()
+        self._c.check(self.L.qi_search_step(self.h, ctypes.byref(info)))
+        self.kernel_ms += info.kernel_ms
+        self.launches += 1
+
+    def frontier(self) -> int:
+        return int(self.L.qi_search_frontier(self.h))
+
+    def keep_slice(self, begin, end):
+        self._c.check(self.L.qi_search_keep_slice(self.h, begin, end))
+
+    def export(self, count, dst):
+        self._c.check(self.L.qi_search_export(self.h, count, ctypes.c_void_p(dst.data_ptr())))
+
+    def import_(self, count, src):
+        self._c.check(self.L.qi_search_import(self.h, count, ctypes.c_void_p(src.data_ptr())))
+
+    def local_best(self):
+        k = (ctypes.c_uint32 * self.key_words)()
+        d = ctypes.c_uint32()
+        if self.L.qi_search_local_best(self.h, k, ctypes.byref(d)) == 1:
+            return tuple(int(x) for x in k), int(d.value)
+        return None
+
+    def set_best(self, key):
+        k = (ctypes.c_uint32 * self.key_words)(*key[0])
+        self._c.check(self.L.qi_search_set_best(self.h, k, key[1]))
+
+    def reduce(self, key):
+        t = self._c.Totals()
+        if key is None:
+            self._c.check(self.L.qi_search_reduce(self.h, None, 0, ctypes.byref(t)))
+        else:
+            k = (ctypes.c_uint32 * self.key_words)(*key[0])
+            self._c.check(self.L.qi_search_reduce(self.h, k, key[1], ctypes.byref(t)))
+        return {"nodes": t.nodes, "evals": t.evals, "minq": t.minq, "zero_fallback": t.zero_fallback,
+                "rounds": t.rounds}
+
+    def shape(self) -> Dict[str, int]:
+        sh = self._c.Shape()
+        self._c.check(self.L.qi_search_shape(self.h, ctypes.byref(sh)))
+        return {k: int(getattr(sh, k)) for k, _ in self._c.Shape._fields_}
+
+    def witness(self):
+        n = self.fbas.n
+        q1 = (ctypes.c_uint32 * max(n, 1))()
+        q2 = (ctypes.c_uint32 * max(n, 1))()
+        l1, l2 = ctypes.c_uint32(), ctypes.c_uint32()
+        self._c.check(self.L.qi_search_witness(self.h, q1, ctypes.byref(l1), q2, ctypes.byref(l2)))
+        return list(q1)[: l1.value], list(q2)[: l2.value]
+
+
+# ------------------------------------------------------------------------------------
+# Host-side planning (pure functions, unit-tested)
+# ------------------------------------------------------------------------------------
+def slice_bounds(total: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous preorder-respecting slice of the initial frontier for `rank`."""
+    base, extra = divmod(total, world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def plan_rebalance(sizes: Sequence[int], min_move: int = 1) -> List[Tuple[int, int, int]]:
+    """Moves (src, dst, count) that bring every rank to within one unit of the mean.
+    Deterministic: every rank computes the same plan from the same gathered sizes."""
+    world = len(sizes)
+    total = sum(sizes)
+    target = [total // world + (1 if r < total % world else 0) for r in range(world)]
+    excess = [(s - t, r) for r, (s, t) in enumerate(zip(sizes, target))]
+    donors = sorted([(e, r) for e, r in excess if e > 0], reverse=True)
+    takers = sorted([(-e, r) for e, r in excess if e < 0], reverse=True)
+    moves = []
+    i = j = 0
+    donors = [list(x) for x in donors]
+    takers = [list(x) for x in takers]
+    while i < len(donors) and j < len(takers):
+        c = min(donors[i][0], takers[j][0])
+        if c >= min_move:
+            moves.append((donors[i][1], takers[j][1], c))
+        donors[i][0] -= c
+        takers[j][0] -= c
+        if donors[i][0] == 0:
+            i += 1
+        if takers[j][0] == 0:
+            j += 1
+    return moves
+
+
+def best_of(keys: Sequence[Optional[Key]]) -> Optional[Key]:
+    ks = [k for k in keys if k is not None]
+    return min(ks) if ks else None
+
+
+def needs_rebalance(sizes: Sequence[int], lanes: int) -> bool:
+    """Rebalance when some rank would idle part of its GPU while another holds surplus."""
+    if max(sizes) == 0:
+        return False
+    lo, hi = min(sizes), max(sizes)
+    return lo < lanes and hi > 2 * max(lo, 1)
+
+
+# ------------------------------------------------------------------------------------
+# The multi-rank driver
+# ------------------------------------------------------------------------------------
+@dataclass
+class DistResult:
+    verdict: bool
+    nodes: int
+    evals: int
+    minq: int
+    zero_fallback: int
+    rounds: int
+    q1: List[int] = field(default_factory=list)
+    q2: List[int] = field(default_factory=list)
+    launches: int = 0
+    moved_units: int = 0
+    wall_s: float = 0.0
+
+
+def _gather_state(be: SearchBackend, device, group) -> Tuple[List[int], List[Optional[Key]]]:
+    kw = be.key_words
+    best = be.local_best()
+    row = [be.frontier(), 1 if best else 0, best[1] if best else 0] + (list(best[0]) if best else [0] * kw)
+    t = torch.tensor(row, dtype=torch.int64, device=device)
+    world = dist.get_world_size(group)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t, group=group)
+    sizes, keys = [], []
+    for o in out:
+        v = [int(x) for x in o.tolist()]
+        sizes.append(v[0])
+        keys.append((tuple(v[3:3 + kw]), v[2]) if v[1] else None)
+    return sizes, keys
+
+
+def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int = 1 << 17,
+                       rebalance: bool = True, min_move: int = 64) -> DistResult:
+    """Run one full search across the ranks of `group`; every rank returns the result."""
+    if dist.is_available() and dist.is_initialized():
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+    else:
+        rank, world = 0, 1
+    t0 = time.perf_counter()
+    be.restart()
+    launches = 0
+    # (1) only rank 0 holds the root (cpp:393); the rebalancing below hands out units as
+    # soon as its frontier grows.  (Splitting a frontier every rank expanded "identically"
+    # would be unsound: the device spill order depends on atomics and differs per run.)
+    if rank != 0:
+        be.clear()
+    moved = 0
+    # (2) independent launches; exchange sizes/best keys; rebalance surplus frontier
+    while True:
+        if be.frontier():
+            be.step()
+            launches += 1
+        sizes, keys = _gather_state(be, device, group) if world > 1 else ([be.frontier()], [be.local_best()])
+        best = best_of(keys)
+        if best is not None:
+            be.set_best(best)
+        if sum(sizes) == 0:
+            break
+        if world > 1 and rebalance and needs_rebalance(sizes, lanes):
+            for src, dst, cnt in plan_rebalance(sizes, min_move=min_move):
+                nbytes = cnt * be.unit_bytes
+                if rank == src:
+                    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+                    be.export(cnt, buf)
+                    dist.send(buf, dst, group=group)
+                elif rank == dst:
+                    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+                    dist.recv(buf, src, group=group)
+                    be.import_(cnt, buf)
+                moved += cnt
+    # (3) preorder-exact totals against the global best witness
+    sizes, keys = _gather_state(be, device, group) if world > 1 else ([0], [be.local_best()])
+    best = best_of(keys)
+    loc = be.reduce(best)
+    vec = torch.tensor([loc["nodes"], loc["evals"], loc["minq"], loc["zero_fallback"], loc["rounds"], launches],
+                       dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(vec, group=group)
+    tot = [int(x) for x in vec.tolist()]
+    q1: List[int] = []
+    q2: List[int] = []
+    if best is not None:
+        owner = keys.index(best)
+        if world > 1:
+            n = be.fbas.n if hasattr(be, "fbas") else 0
+            w = torch.full((2, max(n, 1) + 1), -1, dtype=torch.int64, device=device)
+            if rank == owner:
+                a, b = be.witness()
+                w[0, 0], w[1, 0] = len(a), len(b)
+                if a:
+                    w[0, 1:1 + len(a)] = torch.tensor(a, dtype=torch.int64, device=device)
+                if b:
+                    w[1, 1:1 + len(b)] = torch.tensor(b, dtype=torch.int64, device=device)
+            dist.broadcast(w, owner, group=group)
+            wl = w.tolist()
+            q1 = [int(x) for x in wl[0][1:1 + int(wl[0][0])]]
+            q2 = [int(x) for x in wl[1][1:1 + int(wl[1][0])]]
+        else:
+            q1, q2 = be.witness()
+    return DistResult(verdict=best is None, nodes=tot[0], evals=tot[1], minq=tot[2], zero_fallback=tot[3],
+                      rounds=tot[4], q1=q1, q2=q2, launches=tot[5], moved_units=moved,
+                      wall_s=time.perf_counter() - t0)
