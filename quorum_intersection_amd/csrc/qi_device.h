@@ -32,6 +32,7 @@ struct SearchConfig {
   uint32_t max_blocks = 0;       // 0 = CUs * 8
   uint32_t grow_budget = 48;     // per-lane node budget while the frontier is small
   uint32_t run_budget = 4096;    // per-lane node budget once the frontier fills the GPU
+  uint32_t grace = 64;           // per-lane steps after the unit queue runs dry
   uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output)
   bool keep_log = true;          // keep per-segment records for preorder-exact counts
 };

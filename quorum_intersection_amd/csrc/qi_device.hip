@@ -63,6 +63,14 @@ struct LocalDev {
   uint32_t T, R, G, m;
 };
 
+// Wave-uniform tables are read through the constant address space so the compiler emits
+// scalar loads (s_load into SGPRs, consumed directly by v_and/v_bcnt) instead of vector
+// loads with a uniform address (SQ_INSTS_VMEM dominated the first profile, r01).
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* K(const T* p) {
+  return (const __attribute__((address_space(4))) T*)p;
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -73,9 +81,9 @@ template <int MW, int TW>
 __device__ __forceinline__ uint32_t extra_terms(const LocalDev& f, uint32_t t, const uint32_t (&X)[MW],
                                                 const uint32_t (&sb)[TW]) {
   uint32_t c = 0;
-  const uint32_t e0 = f.extra_off[t], e1 = f.extra_off[t + 1];
+  const uint32_t e0 = K(f.extra_off)[t], e1 = K(f.extra_off)[t + 1];
   for (uint32_t e = e0; e < e1; ++e) {
-    const uint32_t src = f.extra_src[e], msk = f.extra_mask[e];
+    const uint32_t src = K(f.extra_src)[e], msk = K(f.extra_mask)[e];
     uint32_t word = 0;
 #pragma unroll
     for (int w = 0; w < MW; ++w) word = (src == (uint32_t)w) ? X[w] : word;
@@ -109,12 +117,12 @@ __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32
       for (uint32_t t = tb; t < te; ++t) {
         uint32_t c = 0;
 #pragma unroll
-        for (int w = 0; w < MW; ++w) c += __popc(X[w] & f.vmask[t * MW + w]);
+        for (int w = 0; w < MW; ++w) c += __popc(X[w] & K(f.vmask)[t * MW + w]);
 #pragma unroll
-        for (int w = 0; w <= tw; ++w) c += __popc(sb[w] & f.cmask[t * TW + w]);
-        const uint32_t fl = f.flags[t];
+        for (int w = 0; w <= tw; ++w) c += __popc(sb[w] & K(f.cmask)[t * TW + w]);
+        const uint32_t fl = K(f.flags)[t];
         if (fl & 2u) c += extra_terms<MW, TW>(f, t, X, sb);
-        const int32_t th = pol ? f.thr[2 * t + 1] : f.thr[2 * t];
+        const int32_t th = pol ? K(f.thr)[2 * t + 1] : K(f.thr)[2 * t];
         const bool s = (fl & 1u) ? (c == 0u) : ((int32_t)c >= th);
         sb[tw] |= (uint32_t)s << (t - tb);
       }
@@ -123,13 +131,13 @@ __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32
 #pragma unroll
     for (int w = 0; w < MW; ++w) Xn[w] = 0;
     for (uint32_t r = 0; r < f.R; ++r) {
-      const uint32_t tn = f.root_tn[r];
+      const uint32_t tn = K(f.root_tn)[r];
       uint32_t word = sb[0];
 #pragma unroll
       for (int w = 1; w < TW; ++w) word = ((tn >> 5) == (uint32_t)w) ? sb[w] : word;
       const uint32_t sel = 0u - ((word >> (tn & 31u)) & 1u);
 #pragma unroll
-      for (int w = 0; w < MW; ++w) Xn[w] |= f.root_users[r * MW + w] & sel;
+      for (int w = 0; w < MW; ++w) Xn[w] |= K(f.root_users)[r * MW + w] & sel;
     }
     bool same = true;
 #pragma unroll
@@ -153,15 +161,15 @@ __device__ __forceinline__ uint32_t best_node(const LocalDev& f, const uint32_t 
   for (uint32_t g = 0; g < f.G; ++g) {
     uint32_t deg = 0, low = 0xFFFFFFFFu;
 #pragma unroll
-    for (int w = 0; w < MW; ++w) deg += __popc(Q[w] & f.grp_col[g * MW + w]);
-    const uint32_t e0 = f.grp_extra_off[g], e1 = f.grp_extra_off[g + 1];
+    for (int w = 0; w < MW; ++w) deg += __popc(Q[w] & K(f.grp_col)[g * MW + w]);
+    const uint32_t e0 = K(f.grp_extra_off)[g], e1 = K(f.grp_extra_off)[g + 1];
     for (uint32_t e = e0; e < e1; ++e) {
 #pragma unroll
-      for (int w = 0; w < MW; ++w) deg += __popc(Q[w] & f.grp_extra[e * MW + w]);
+      for (int w = 0; w < MW; ++w) deg += __popc(Q[w] & K(f.grp_extra)[e * MW + w]);
     }
 #pragma unroll
     for (int w = MW - 1; w >= 0; --w) {
-      const uint32_t c = Q[w] & ~D[w] & f.grp_members[g * MW + w];
+      const uint32_t c = Q[w] & ~D[w] & K(f.grp_members)[g * MW + w];
       low = c ? (uint32_t)w * 32u + (uint32_t)__builtin_ctz(c) : low;
     }
     const bool better = (low != 0xFFFFFFFFu) && (deg > bestdeg || (deg == bestdeg && low < bestv));
@@ -209,6 +217,7 @@ struct SearchArgs {
   unsigned long long* totals;    // nodes, evals, minq, zero_fallback, rounds, units_fetched
   unsigned long long* best64;    // exact preorder key when MW == 1
   uint32_t budget;
+  uint32_t grace;                // extra steps per lane once the unit queue is dry
   uint32_t evict_max;
   uint32_t half_m;
   uint32_t has_best;             // host-known best key (multiword) for pruning
@@ -290,6 +299,9 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
   bool has = false, done = false;
   uint32_t nst = 0, sbase = 0;
   uint32_t steps = 0, evictions = 0;
+  uint32_t limit = a.budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
+  bool dry = false;
+  uint32_t iter = 0;
   // current segment (one per fetched unit)
   bool seg_open = false;
   uint32_t seg_idx = 0, seg_depth = 0, seg_count = 0, seg_evals = 0, seg_minq = 0, seg_zfb = 0;
@@ -413,7 +425,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
       }
       if (!has && nst == 0) {
         if (seg_open) close_segment();
-        if (steps >= a.budget) done = true;
+        if (steps >= limit) done = true;
       }
     }
 
@@ -472,6 +484,19 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
     if (ring_dead && need) done = true;
     if (!__any(has)) break;
 
+    // once no unit is left to fetch anywhere, give every lane a short grace period and
+    // then spill: the next launch spreads the remaining subtrees over all lanes instead
+    // of letting a few lanes grind through deep subtrees while the rest idle.
+    if (!dry && ((iter++ & 15u) == 0u || ring_dead)) {
+      uint32_t h = 0;
+      if (lane == 0) h = __hip_atomic_load(&a.counters[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      h = __shfl(h, 0);
+      if (ring_dead || h >= a.n_in) {
+        dry = true;
+        limit = min(limit, steps + a.grace);
+      }
+    }
+
     // refresh the device-side best key (exact 64-bit preorder key when MW == 1)
     if (MW == 1) {
       uint64_t b = 0;
@@ -481,7 +506,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
 
     // ---- (3) budget exhausted: spill current node + stack to the next frontier --------
     {
-      const bool spill = has && (steps >= a.budget || evictions >= a.evict_max);
+      const bool spill = has && (steps >= limit || evictions >= a.evict_max);
       if (__any(spill)) {
         uint32_t total = 0;
         const uint32_t n = spill ? 1u + nst : 0u;
@@ -1148,6 +1173,7 @@ class SearchDeviceImpl : public SearchDevice {
     a.totals = totals_;
     a.best64 = best64_;
     a.budget = budget;
+    a.grace = cfg_.grace;
     a.evict_max = cfg_.evict_max;
     a.half_m = m_ / 2;
     a.has_best = has_best_ ? 1u : 0u;
