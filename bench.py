@@ -201,6 +201,9 @@ def main():
             "kernel": "search_kernel",
             "avg_launch_ms": avg_launch_ms,
             "launches_per_step": launches_all / args.steps / world,
+            "lane_occupancy": res.nodes / max(64 * res.wave_iters, 1),
+            "coop_phase_frac": res.coop_phases / max(res.wave_iters, 1),
+            "units_per_step": res.units,
         },
         "time_to_verdict_s": time_to_verdict,
         "time_to_verdict_note": "N=1 path from JSON text in host memory: parse, SCCs, flatten, upload, solve",

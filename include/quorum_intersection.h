@@ -143,6 +143,9 @@ typedef struct {
 
 typedef struct {
   uint64_t nodes, evals, minq, zero_fallback, rounds;
+  uint64_t units;        /* frontier units fetched (all launches) */
+  uint64_t wave_iters;   /* search-loop iterations summed over wavefronts */
+  uint64_t coop_phases;  /* iterations that ran the cooperative minimality phase */
 } qi_totals;
 
 /* Shape of the flattened searched SCC (for work accounting). */

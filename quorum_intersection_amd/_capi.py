@@ -80,7 +80,7 @@ class Shape(ctypes.Structure):
 
 class Totals(ctypes.Structure):
     _fields_ = [("nodes", c_uint64), ("evals", c_uint64), ("minq", c_uint64), ("zero_fallback", c_uint64),
-                ("rounds", c_uint64)]
+                ("rounds", c_uint64), ("units", c_uint64), ("wave_iters", c_uint64), ("coop_phases", c_uint64)]
 
 
 # name -> (restype, argtypes); must match include/quorum_intersection.h exactly

@@ -401,6 +401,9 @@ int qi_search_reduce(qi_search* s, const uint32_t* key, uint32_t depth, qi_total
     out->minq = t.minq;
     out->zero_fallback = t.zero_fallback;
     out->rounds = t.rounds;
+    out->units = t.units;
+    out->wave_iters = t.wave_iters;
+    out->coop_phases = t.coop_phases;
     return QI_OK;
   });
 }

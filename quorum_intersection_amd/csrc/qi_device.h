@@ -48,6 +48,7 @@ struct StepInfo {
 
 struct Totals {
   uint64_t nodes = 0, evals = 0, minq = 0, zero_fallback = 0, rounds = 0;
+  uint64_t units = 0, wave_iters = 0, coop_phases = 0;  // occupancy accounting (unfiltered)
 };
 
 struct Witness {

@@ -46,11 +46,20 @@ constexpr int WAVE = 64;
 // ------------------------------------------------------------------------------------
 // SCC-local TN table (see LocalFlat in qi_internal.h)
 // ------------------------------------------------------------------------------------
+// One packed record per threshold node, read with a single wide scalar load:
+//   [0, MW) validator mask (plane 0) | [MW, MW+TW) child mask (plane 0) |
+//   thr (outside unavailable) | thr (outside available) | invert | has-extra-planes
+// "invert" encodes threshold 0 ("first entry unavailable"): thr = 1 and the test is
+// flipped, so sat = (count >= thr) XOR invert without a branch.
+template <int MW, int TW>
+struct TnRec {
+  static constexpr int RAW = MW + TW + 4;
+  static constexpr int WORDS = RAW <= 8 ? 8 : (RAW <= 16 ? 16 : 32);
+  static constexpr int THR0 = MW + TW, THR1 = MW + TW + 1, INV = MW + TW + 2, EXTRA = MW + TW + 3;
+};
+
 struct LocalDev {
-  const int32_t* thr;          // [T][2]
-  const uint32_t* flags;       // [T]
-  const uint32_t* vmask;       // [T][MW]
-  const uint32_t* cmask;       // [T][TW]
+  const uint32_t* tn;          // [T][TnRec::WORDS]
   const uint32_t* extra_off;   // [T+1]
   const uint32_t* extra_src;
   const uint32_t* extra_mask;
@@ -96,11 +105,13 @@ __device__ __forceinline__ uint32_t extra_terms(const LocalDev& f, uint32_t t, c
 
 // containsQuorum (cpp:140-177) as a Jacobi greatest fixpoint on one lane's masks.
 // X: in = candidate set (nodes ∩ avail within the SCC), out = survivors.
-// pol: 0 = vertices outside the SCC unavailable (cpp:281/184/192/301/658),
-//      1 = available (visitor, cpp:354/368).  Returns true iff survivors != ∅.
-// Same set as the reference's Gauss-Seidel sweep (monotone operator), different rounds.
-template <int MW, int TW>
+// POL 0 = vertices outside the SCC unavailable (cpp:281/184/192/301/658),
+//     1 = available (visitor, cpp:354/368), 2 = per-lane `pol` (cooperative phase).
+// Same set as the reference's Gauss-Seidel sweep for monotone slices (every quorum set
+// has threshold >= 1); threshold-0 inputs are flagged nonmonotone by the host.
+template <int MW, int TW, int POL>
 __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32_t pol, uint32_t& rounds) {
+  using R = TnRec<MW, TW>;
   for (;;) {
     uint32_t any = 0;
 #pragma unroll
@@ -114,17 +125,21 @@ __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32
     for (int tw = 0; tw < TW; ++tw) {
       const uint32_t tb = (uint32_t)tw * 32u;
       const uint32_t te = min(f.T, tb + 32u);
-      for (uint32_t t = tb; t < te; ++t) {
+      const __attribute__((address_space(4))) uint32_t* rec = K(f.tn) + (size_t)tb * R::WORDS;
+#pragma unroll 4
+      for (uint32_t t = tb; t < te; ++t, rec += R::WORDS) {
         uint32_t c = 0;
 #pragma unroll
-        for (int w = 0; w < MW; ++w) c += __popc(X[w] & K(f.vmask)[t * MW + w]);
+        for (int w = 0; w < MW; ++w) c += __popc(X[w] & rec[w]);
 #pragma unroll
-        for (int w = 0; w <= tw; ++w) c += __popc(sb[w] & K(f.cmask)[t * TW + w]);
-        const uint32_t fl = K(f.flags)[t];
-        if (fl & 2u) c += extra_terms<MW, TW>(f, t, X, sb);
-        const int32_t th = pol ? K(f.thr)[2 * t + 1] : K(f.thr)[2 * t];
-        const bool s = (fl & 1u) ? (c == 0u) : ((int32_t)c >= th);
-        sb[tw] |= (uint32_t)s << (t - tb);
+        for (int w = 0; w <= tw; ++w) c += __popc(sb[w] & rec[MW + w]);
+        if (rec[R::EXTRA]) c += extra_terms<MW, TW>(f, t, X, sb);  // multiplicity > 1 (rare)
+        int32_t th;
+        if (POL == 0) th = (int32_t)rec[R::THR0];
+        else if (POL == 1) th = (int32_t)rec[R::THR1];
+        else th = pol ? (int32_t)rec[R::THR1] : (int32_t)rec[R::THR0];
+        const uint32_t bit = (((int32_t)c >= th) ? 1u : 0u) ^ rec[R::INV];
+        sb[tw] |= bit << (t - tb);
       }
     }
     uint32_t Xn[MW];
@@ -285,12 +300,14 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
   uint32_t* co_NE = co_D + MW * WAVE;                           // [MW][64]
   uint32_t* co_VIS = co_NE + MW * WAVE;                         // [MW][64]
   uint32_t* co_off = co_VIS + MW * WAVE;                        // [65] (+pad)
-  uint8_t* dord = (uint8_t*)(co_off + 68);                      // [DMAX][64]
+  uint32_t* uring = co_off + 68;                                // [UW][64] staged units
+  uint8_t* dord = (uint8_t*)(uring + UW * WAVE);                // [DMAX][64]
 
   const uint32_t lane = threadIdx.x;
   const LocalDev& f = a.f;
 #define ST_(lvl, w) st[((lvl) * SE + (w)) * WAVE + lane]
 #define DO_(i) dord[(i) * WAVE + lane]
+#define UR_(w, slot) uring[(w) * WAVE + (slot)]
 
   uint32_t T[MW], D[MW], K[MW];
 #pragma unroll
@@ -310,12 +327,33 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
   for (int w = 0; w < MW; ++w) seg_K[w] = 0;
   uint64_t tot_nodes = 0, tot_evals = 0, tot_minq = 0, tot_zfb = 0, tot_fetched = 0;
   uint32_t rounds = 0;
+  uint32_t wave_iters = 0, coop_phases = 0;  // wave-uniform: occupancy accounting
 
-  // wave-uniform fetch ring: first 64 units of this block are statically assigned
-  uint32_t ring_pos = blockIdx.x * WAVE;
-  uint32_t ring_end = min(a.n_in, ring_pos + (uint32_t)WAVE);
+  // wave-uniform LDS ring of staged units (see (2) below)
+  uint32_t ring_src = 0, ring_cnt = 0, ring_next = 0;
   bool ring_dead = false;
   uint64_t best64 = ~0ull;
+  auto refill = [&](uint32_t base) {  // convergent: every lane stages one unit
+    const uint32_t cnt = min(a.n_in - base, (uint32_t)WAVE);
+    if (lane < cnt) {
+      const uint4* src = (const uint4*)(a.units_in + (size_t)(base + lane) * UW);
+#pragma unroll
+      for (int q = 0; q < UW / 4; ++q) {
+        const uint4 v = src[q];
+        UR_(4 * q + 0, lane) = v.x;
+        UR_(4 * q + 1, lane) = v.y;
+        UR_(4 * q + 2, lane) = v.z;
+        UR_(4 * q + 3, lane) = v.w;
+      }
+    }
+    __syncthreads();
+    ring_src = base;
+    ring_cnt = cnt;
+    ring_next = 0;
+  };
+  // the first 64 units of this block's range are statically assigned (no atomic)
+  if (blockIdx.x * WAVE < a.n_in) refill(blockIdx.x * WAVE);
+  else ring_dead = true;
 
   auto close_segment = [&]() {
     uint32_t* r = a.records + (size_t)seg_idx * RL::WORDS;
@@ -429,11 +467,14 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
       }
     }
 
-    // ---- (2) fetch new units (wave-aggregated, ring of 64) --------------------------
+    // ---- (2) fetch new units from the wave's LDS ring --------------------------------
+    // The ring holds up to 64 units staged by one coalesced refill (one atomic on the
+    // global head + one unit per lane), so the global-load latency is paid once per 64
+    // fetches instead of on every fetch.
     bool need = !done && !has;
     uint64_t nm = __ballot(need);
     while (nm) {
-      if (ring_pos >= ring_end) {
+      if (ring_next >= ring_cnt) {
         if (ring_dead) break;
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(&a.counters[1], (uint32_t)WAVE);
@@ -442,31 +483,29 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
           ring_dead = true;
           break;
         }
-        ring_pos = base;
-        ring_end = min(a.n_in, base + (uint32_t)WAVE);
+        refill(base);
       }
-      const uint32_t avail = ring_end - ring_pos;
+      const uint32_t avail = ring_cnt - ring_next;
       const uint32_t r = rank_in(nm);
       if (need && r < avail) {
-        const uint32_t idx = ring_pos + r;
-        const uint32_t* u = a.units_in + (size_t)idx * UW;
+        const uint32_t slot = ring_next + r;
         uint32_t UK[MW];
 #pragma unroll
         for (int w = 0; w < MW; ++w) {
-          T[w] = u[UL::T_ + w];
-          D[w] = u[UL::D_ + w];
-          UK[w] = u[UL::K_ + w];
+          T[w] = UR_(UL::T_ + w, slot);
+          D[w] = UR_(UL::D_ + w, slot);
+          UK[w] = UR_(UL::K_ + w, slot);
         }
-        const uint32_t ud = u[UL::DEPTH];
-        dlen = u[UL::DLEN];
+        const uint32_t ud = UR_(UL::DEPTH, slot);
+        dlen = UR_(UL::DLEN, slot);
         for (uint32_t i = 0; i < (dlen + 3) / 4; ++i) {
-          const uint32_t word = u[UL::ORD + i];
+          const uint32_t word = UR_(UL::ORD + i, slot);
 #pragma unroll
           for (uint32_t j = 0; j < 4; ++j)
             if (i * 4 + j < dlen) DO_(i * 4 + j) = (uint8_t)(word >> (8 * j));
         }
         ++tot_fetched;
-        seg_idx = idx;
+        seg_idx = ring_src + slot;
         seg_open = true;
         seg_count = seg_evals = seg_minq = seg_zfb = 0;
 #pragma unroll
@@ -478,30 +517,30 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
         if (pruned(UK, ud)) close_segment();  // zero record
         else has = true;
       }
-      ring_pos += min((uint32_t)__popcll(nm), avail);
+      ring_next += min((uint32_t)__popcll(nm), avail);
       nm = __ballot(need);
     }
     if (ring_dead && need) done = true;
     if (!__any(has)) break;
 
-    // once no unit is left to fetch anywhere, give every lane a short grace period and
-    // then spill: the next launch spreads the remaining subtrees over all lanes instead
-    // of letting a few lanes grind through deep subtrees while the rest idle.
-    if (!dry && ((iter++ & 15u) == 0u || ring_dead)) {
+    // Every 32 iterations poll the global head and the device-side best key (one
+    // blocking global load pair, kept off the per-iteration path).  Once no unit is left
+    // to fetch anywhere, every lane gets a short grace period and then spills: the next
+    // launch spreads the remaining subtrees over all lanes instead of letting a few lanes
+    // grind through deep subtrees while the rest idle.
+    if ((iter++ & 31u) == 0u || (ring_dead && !dry)) {
       uint32_t h = 0;
-      if (lane == 0) h = __hip_atomic_load(&a.counters[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t b = ~0ull;
+      if (lane == 0) {
+        h = __hip_atomic_load(&a.counters[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (MW == 1) b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       h = __shfl(h, 0);
-      if (ring_dead || h >= a.n_in) {
+      best64 = __shfl(b, 0);
+      if (!dry && (ring_dead || h >= a.n_in)) {
         dry = true;
         limit = min(limit, steps + a.grace);
       }
-    }
-
-    // refresh the device-side best key (exact 64-bit preorder key when MW == 1)
-    if (MW == 1) {
-      uint64_t b = 0;
-      if (lane == 0) b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      best64 = __shfl(b, 0);
     }
 
     // ---- (3) budget exhausted: spill current node + stack to the next frontier --------
@@ -523,6 +562,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
     }
 
     // ---- (4) one search node per active lane (cpp:258-345) ---------------------------
+    ++wave_iters;
     bool pending = false;
     bool active = has;
     if (has) {
@@ -539,7 +579,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
     uint32_t X[MW];
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = active ? D[w] : 0u;
-    const bool dq = gfp<MW, TW>(f, X, 0u, rounds);  // cpp:281
+    const bool dq = gfp<MW, TW, 0>(f, X, 0u, rounds);  // cpp:281
     if (active) {
       ++seg_evals;
       pending = dq;
@@ -547,7 +587,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
     const bool active2 = active && !dq;
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = active2 ? (T[w] | D[w]) : 0u;
-    const bool qne = gfp<MW, TW>(f, X, 0u, rounds);  // cpp:301
+    const bool qne = gfp<MW, TW, 0>(f, X, 0u, rounds);  // cpp:301
     bool push = false;
     uint32_t pb = 0;
     if (active2) {
@@ -598,6 +638,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
     // ---- (5) quorum leaves: isMinimalQuorum + visitor, wave-cooperative --------------
     const uint64_t pm = __ballot(pending);
     if (pm) {
+      ++coop_phases;
       const uint32_t npend = (uint32_t)__popcll(pm);
       const uint32_t r = rank_in(pm);
       uint32_t nj = pending ? dlen + 1u : 0u;
@@ -663,7 +704,7 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
           else Y[w] = Dr[w];
         }
         if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
-        const bool ne = gfp<MW, TW>(f, Y, vis ? 1u : 0u, rounds);
+        const bool ne = gfp<MW, TW, 2>(f, Y, vis ? 1u : 0u, rounds);
         if (act && !vis && ne) atomicOr(&co_NE[(v >> 5) * WAVE + o], 1u << (v & 31u));
         if (vis) {
 #pragma unroll
@@ -727,7 +768,8 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
 
   // units claimed by this wave's ring but never fetched: carry them over unchanged
   {
-    const uint32_t left = (ring_pos < ring_end) ? ring_end - ring_pos : 0u;
+    const uint32_t ring_pos = ring_src + ring_next;
+    const uint32_t left = (ring_next < ring_cnt) ? ring_cnt - ring_next : 0u;
     if (left) {
       uint32_t base = 0;
       if (lane == 0) base = atomicAdd(&a.counters[0], left);
@@ -766,9 +808,12 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
     atomicAdd(&a.totals[3], (unsigned long long)tot_zfb);
     atomicAdd(&a.totals[4], (unsigned long long)tr);
     atomicAdd(&a.totals[5], (unsigned long long)tot_fetched);
+    atomicAdd(&a.totals[6], (unsigned long long)wave_iters);
+    atomicAdd(&a.totals[7], (unsigned long long)coop_phases);
   }
 #undef ST_
 #undef DO_
+#undef UR_
 }
 
 // Zero-record the units never claimed from the global head (host carries them over).
@@ -1053,31 +1098,34 @@ class SearchDeviceImpl : public SearchDevice {
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
-    // pad TN tables to the template's word counts
+    // pack one record per TN (TnRec layout), padded to the template's word counts
+    using RC = dev::TnRec<MW, TW>;
     const uint32_t T = f.T;
-    std::vector<uint32_t> vmask((size_t)T * MW, 0), cmask((size_t)T * TW, 0);
+    std::vector<uint32_t> rec((size_t)std::max<uint32_t>(T, 1) * RC::WORDS, 0);
     for (uint32_t t = 0; t < T; ++t) {
-      for (uint32_t w = 0; w < f.mw; ++w) vmask[(size_t)t * MW + w] = f.vmask[(size_t)t * f.mw + w];
-      for (uint32_t w = 0; w < f.tw; ++w) cmask[(size_t)t * TW + w] = f.cmask[(size_t)t * f.tw + w];
+      uint32_t* r = &rec[(size_t)t * RC::WORDS];
+      for (uint32_t w = 0; w < f.mw; ++w) r[w] = f.vmask[(size_t)t * f.mw + w];
+      for (uint32_t w = 0; w < f.tw; ++w) r[MW + w] = f.cmask[(size_t)t * f.tw + w];
+      const bool inv = (f.flags[t] & 1u) != 0;
+      r[RC::THR0] = inv ? 1u : (uint32_t)f.thr[2 * t];
+      r[RC::THR1] = inv ? 1u : (uint32_t)f.thr[2 * t + 1];
+      r[RC::INV] = inv ? 1u : 0u;
+      r[RC::EXTRA] = (f.flags[t] & 2u) ? 1u : 0u;
     }
     std::vector<uint32_t> extra_src = f.extra_src;
-    for (auto& s : extra_src)
-      if (s >= f.mw) s = s - f.mw + MW;  // re-base TN-sat words after padding
+    for (auto& x : extra_src)
+      if (x >= f.mw) x = x - f.mw + MW;  // re-base TN-sat words after padding
     auto pad_rows = [&](const std::vector<uint32_t>& v, size_t rows) {
       std::vector<uint32_t> o(rows * MW, 0);
       for (size_t r = 0; r < rows; ++r)
         for (uint32_t w = 0; w < f.mw; ++w) o[r * MW + w] = v[r * f.mw + w];
       return o;
     };
-    std::vector<int32_t> thr = f.thr;
     d_.T = T;
     d_.R = f.R;
     d_.G = f.G;
     d_.m = f.m;
-    keep(d_.thr = dupload(thr, stream_));
-    keep(d_.flags = dupload(f.flags, stream_));
-    keep(d_.vmask = dupload(vmask, stream_));
-    keep(d_.cmask = dupload(cmask, stream_));
+    keep(d_.tn = dupload(rec, stream_));
     keep(d_.extra_off = dupload(f.extra_off, stream_));
     keep(d_.extra_src = dupload(extra_src, stream_));
     keep(d_.extra_mask = dupload(f.extra_mask, stream_));
@@ -1104,7 +1152,7 @@ class SearchDeviceImpl : public SearchDevice {
     unsigned long long inf = ~0ull;
     HIP_CHECK(hipMemcpyAsync(best64_, &inf, 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
-    shm_ = (size_t)(SMAX * (MW + 1) * 64 + 3 * MW * 64 + 68) * 4 + (size_t)UL::DMAX * 64;
+    shm_ = (size_t)(SMAX * (MW + 1) * 64 + 3 * MW * 64 + 68 + UL::WORDS * 64) * 4 + (size_t)UL::DMAX * 64;
     shm_ = (shm_ + 15) / 16 * 16;
     HIP_CHECK(hipFuncSetAttribute((const void*)dev::search_kernel<MW, TW, SMAX>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
@@ -1296,7 +1344,11 @@ class SearchDeviceImpl : public SearchDevice {
     t.evals = r[1];
     t.minq = r[2];
     t.zero_fallback = r[3];
-    t.rounds = running_totals().rounds;
+    const Totals rt = running_totals();
+    t.rounds = rt.rounds;
+    t.units = rt.units;
+    t.wave_iters = rt.wave_iters;
+    t.coop_phases = rt.coop_phases;
     return t;
   }
 
@@ -1311,6 +1363,9 @@ class SearchDeviceImpl : public SearchDevice {
     t.minq = r[2];
     t.zero_fallback = r[3];
     t.rounds = r[4];
+    t.units = r[5];
+    t.wave_iters = r[6];
+    t.coop_phases = r[7];
     return t;
   }
 

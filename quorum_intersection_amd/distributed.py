@@ -139,7 +139,7 @@ class DeviceSearch(SearchBackend):
             k = (ctypes.c_uint32 * self.key_words)(*key[0])
             self._c.check(self.L.qi_search_reduce(self.h, k, key[1], ctypes.byref(t)))
         return {"nodes": t.nodes, "evals": t.evals, "minq": t.minq, "zero_fallback": t.zero_fallback,
-                "rounds": t.rounds}
+                "rounds": t.rounds, "units": t.units, "wave_iters": t.wave_iters, "coop_phases": t.coop_phases}
 
     def shape(self) -> Dict[str, int]:
         sh = self._c.Shape()
@@ -220,6 +220,9 @@ class DistResult:
     launches: int = 0
     moved_units: int = 0
     wall_s: float = 0.0
+    units: int = 0
+    wave_iters: int = 0
+    coop_phases: int = 0
 
 
 def _gather_state(be: SearchBackend, device, group) -> Tuple[List[int], List[Optional[Key]]]:
@@ -281,7 +284,8 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
     sizes, keys = _gather_state(be, device, group) if world > 1 else ([0], [be.local_best()])
     best = best_of(keys)
     loc = be.reduce(best)
-    vec = torch.tensor([loc["nodes"], loc["evals"], loc["minq"], loc["zero_fallback"], loc["rounds"], launches],
+    vec = torch.tensor([loc["nodes"], loc["evals"], loc["minq"], loc["zero_fallback"], loc["rounds"], launches,
+                        loc.get("units", 0), loc.get("wave_iters", 0), loc.get("coop_phases", 0)],
                        dtype=torch.int64, device=device)
     if world > 1:
         dist.all_reduce(vec, group=group)
@@ -308,4 +312,4 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
             q1, q2 = be.witness()
     return DistResult(verdict=best is None, nodes=tot[0], evals=tot[1], minq=tot[2], zero_fallback=tot[3],
                       rounds=tot[4], q1=q1, q2=q2, launches=tot[5], moved_units=moved,
-                      wall_s=time.perf_counter() - t0)
+                      wall_s=time.perf_counter() - t0, units=tot[6], wave_iters=tot[7], coop_phases=tot[8])
