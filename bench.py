@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--grow-budget", type=int, default=0)
     ap.add_argument("--run-budget", type=int, default=0)
     ap.add_argument("--max-blocks", type=int, default=0)
+    ap.add_argument("--jit", type=int, default=2,
+                    help="0 auto, 1 table-interpreting kernel only, 2 run-time specialised kernel (default)")
     args = ap.parse_args()
 
     import torch
@@ -105,10 +107,10 @@ def main():
     # ---- time-to-verdict from JSON text (host parse + flatten + upload + solve), N=1 path
     t0 = time.perf_counter()
     fb = qa.FBAS(text, device=local)
-    ttv_res = fb.solve_stats(args.grow_budget, args.run_budget, args.max_blocks)
+    ttv_res = fb.solve_stats(args.grow_budget, args.run_budget, args.max_blocks)  # jit auto (CLI default)
     time_to_verdict = time.perf_counter() - t0
 
-    be = DeviceSearch(fb, args.grow_budget, args.run_budget, args.max_blocks)
+    be = DeviceSearch(fb, args.grow_budget, args.run_budget, args.max_blocks, jit=args.jit)
     shape = be.shape()
     sccs = fb.sccs()
     scc_masks = qa.masks_from_sets(sccs, fb.n)
@@ -119,6 +121,7 @@ def main():
 
     for _ in range(args.warmup):
         one_step()
+    specialised = be.wait_jit()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -198,7 +201,7 @@ def main():
             "unit": "Tops/s (int32 lane-ops)",
             "frac": achieved / VALU_PEAK_TOPS,
             "traffic": traffic,
-            "kernel": "search_kernel",
+            "kernel": "qi_search_spec (run-time specialised search_kernel)" if specialised else "search_kernel",
             "avg_launch_ms": avg_launch_ms,
             "launches_per_step": launches_all / args.steps / world,
             "lane_occupancy": res.nodes / max(64 * res.wave_iters, 1),

@@ -83,6 +83,8 @@ typedef struct {
   uint32_t grow_budget;    /* 0 = default: per-lane node budget while the frontier grows */
   uint32_t run_budget;     /* 0 = default: per-lane node budget at full occupancy */
   uint32_t max_blocks;     /* 0 = default (8 wavefronts per CU) */
+  uint32_t jit;            /* run-time specialised search kernel: 0 auto (background compile
+                              once a search needs >= 3 launches), 1 off, 2 before launch 1 */
 } qi_solve_opts;
 
 typedef struct {
@@ -107,7 +109,7 @@ typedef struct {
                               reference's fixpoints then depend on its sweep order, which
                               at cpp:301 is libstdc++ unordered_set iteration order; the
                               device search uses Jacobi rounds there (parity unpinned) */
-  uint32_t reserved;
+  uint32_t jit_launches;   /* launches that ran the run-time specialised kernel */
 } qi_solve_result;
 
 /* q1, q2: caller buffers of n_vertices entries (may be NULL).  q1 = disjoint quorum
@@ -132,6 +134,7 @@ void qi_free(void* p);
  * ------------------------------------------------------------------------------- */
 typedef struct {
   uint32_t grow_budget, run_budget, max_blocks; /* 0 = defaults */
+  uint32_t jit;                                  /* as qi_solve_opts.jit */
 } qi_search_opts;
 
 typedef struct {
@@ -139,6 +142,8 @@ typedef struct {
   uint32_t budget, blocks;
   uint64_t new_witnesses;
   double kernel_ms;
+  uint32_t specialized;  /* 1 if this launch ran the run-time specialised kernel */
+  uint32_t pad;
 } qi_step_info;
 
 typedef struct {
@@ -159,6 +164,10 @@ typedef struct {
   uint32_t groups;     /* findBestNode column groups */
   uint32_t extra_terms;
 } qi_shape;
+
+/* Compile (or load from the on-disk cache) the run-time specialised search kernel for
+ * sccs.front() with hipRTC; needs no GPU.  *ms = compile wall time. */
+int qi_fbas_jit_precompile(qi_fbas* f, double* ms);
 
 /* Requires exactly one SCC with a quorum (else QI_ERR_STATE: no search is defined). */
 int qi_search_create(qi_fbas* f, const qi_search_opts* opts, qi_search** out);
@@ -182,6 +191,9 @@ int qi_search_witness(qi_search* s, uint32_t* q1, uint32_t* q1_len, uint32_t* q2
 /* Forget processed segments / best (start a fresh search on the same FBAS). */
 int qi_search_restart(qi_search* s);
 double qi_search_kernel_ms(const qi_search* s);
+/* Block until a background compile of the specialised kernel (if any) has finished;
+ * returns 1 if the next launch will use the specialised kernel. */
+int qi_search_wait_jit(qi_search* s);
 int qi_search_shape(const qi_search* s, qi_shape* out);
 
 #ifdef __cplusplus

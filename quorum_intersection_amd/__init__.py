@@ -123,8 +123,10 @@ class FBAS:
         return [v for v in nodes if v in keep]
 
     # ---- device: solve / search -------------------------------------------------------
-    def solve_stats(self, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0) -> Dict:
-        opts = _capi.SolveOpts(0, grow_budget, run_budget, max_blocks)
+    def solve_stats(self, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0, jit: int = 0) -> Dict:
+        """jit: 0 auto (specialised kernel compiled in the background for long searches),
+        1 table-interpreting kernel only, 2 specialised kernel from the first launch."""
+        opts = _capi.SolveOpts(0, grow_budget, run_budget, max_blocks, jit)
         res = _capi.SolveResult()
         q1 = np.zeros(max(self.n, 1), dtype=np.uint32)
         q2 = np.zeros(max(self.n, 1), dtype=np.uint32)
@@ -135,6 +137,12 @@ class FBAS:
         d["q1"] = [int(x) for x in q1[: res.q1_len]]
         d["q2"] = [int(x) for x in q2[: res.q2_len]]
         return d
+
+    def jit_precompile(self) -> float:
+        """Compile/cache the specialised search kernel for sccs.front() (no GPU needed); ms."""
+        ms = ctypes.c_double()
+        check(lib().qi_fbas_jit_precompile(self._h, ctypes.byref(ms)))
+        return ms.value
 
     def checkMinimalQuorums(self) -> Tuple[bool, List[int], List[int]]:
         """checkMinimalQuorums(sccs.front(), ...) (cpp:348-400): (intersecting, q1, q2)."""

@@ -28,7 +28,8 @@ class QIError(RuntimeError):
 
 
 class SolveOpts(ctypes.Structure):
-    _fields_ = [("tiebreak", c_uint32), ("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32)]
+    _fields_ = [("tiebreak", c_uint32), ("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32),
+                ("jit", c_uint32)]
 
 
 class SolveResult(ctypes.Structure):
@@ -52,12 +53,12 @@ class SolveResult(ctypes.Structure):
         ("t_search_ms", c_double),
         ("t_kernel_ms", c_double),
         ("nonmonotone", c_uint32),
-        ("reserved", c_uint32),
+        ("jit_launches", c_uint32),
     ]
 
 
 class SearchOpts(ctypes.Structure):
-    _fields_ = [("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32)]
+    _fields_ = [("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32), ("jit", c_uint32)]
 
 
 class StepInfo(ctypes.Structure):
@@ -69,6 +70,8 @@ class StepInfo(ctypes.Structure):
         ("blocks", c_uint32),
         ("new_witnesses", c_uint64),
         ("kernel_ms", c_double),
+        ("specialized", c_uint32),
+        ("pad", c_uint32),
     ]
 
 
@@ -120,6 +123,8 @@ SIGNATURES = {
     "qi_search_restart": (c_int, [c_void_p]),
     "qi_search_kernel_ms": (c_double, [c_void_p]),
     "qi_search_shape": (c_int, [c_void_p, POINTER(Shape)]),
+    "qi_fbas_jit_precompile": (c_int, [c_void_p, POINTER(c_double)]),
+    "qi_search_wait_jit": (c_int, [c_void_p]),
 }
 
 _lib = None

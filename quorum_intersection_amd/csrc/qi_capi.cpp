@@ -96,8 +96,9 @@ std::vector<uint32_t> scc_quorum_check(qi_fbas* f, std::vector<std::vector<uint3
   return with;
 }
 
-qi::SearchConfig make_cfg(uint32_t grow, uint32_t run, uint32_t blocks) {
+qi::SearchConfig make_cfg(uint32_t grow, uint32_t run, uint32_t blocks, uint32_t jit = 0) {
   qi::SearchConfig c;
+  c.jit = jit;
   if (grow) c.grow_budget = grow;
   if (run) c.run_budget = run;
   if (blocks) c.max_blocks = blocks;
@@ -110,6 +111,7 @@ struct SearchOutcome {
   qi::Totals totals;
   std::vector<uint32_t> q1, q2;  // global indices
   uint64_t launches = 0;
+  uint64_t jit_launches = 0;
   double kernel_ms = 0;
 };
 
@@ -130,6 +132,7 @@ SearchOutcome run_search(qi_fbas* f, const qi::SearchConfig& cfg) {
     for (uint32_t v : w.q2_local) o.q2.push_back(scc[v]);
   }
   o.launches = sd->launches();
+  o.jit_launches = sd->specialized_launches();
   o.kernel_ms = sd->sum_kernel_ms();
   return o;
 }
@@ -212,12 +215,13 @@ int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32
     }
     res->searched = 1;
     qi::SearchConfig cfg = make_cfg(opts ? opts->grow_budget : 0, opts ? opts->run_budget : 0,
-                                    opts ? opts->max_blocks : 0);
+                                    opts ? opts->max_blocks : 0, opts ? opts->jit : 0);
     auto t1 = std::chrono::steady_clock::now();
     SearchOutcome o = run_search(f, cfg);
     res->t_search_ms = ms_since(t1);
     res->t_kernel_ms = o.kernel_ms;
     res->launches = o.launches;
+    res->jit_launches = (uint32_t)o.jit_launches;
     res->nodes = o.totals.nodes;
     res->evals += o.totals.evals;
     res->minq = o.totals.minq;
@@ -320,7 +324,7 @@ int qi_search_create(qi_fbas* f, const qi_search_opts* opts, qi_search** out) {
     s->lf = qi::flatten_local(f->g, f->sccs.members.front());
     s->sd = qi::make_search_device(f->device, s->lf,
                                    make_cfg(opts ? opts->grow_budget : 0, opts ? opts->run_budget : 0,
-                                            opts ? opts->max_blocks : 0));
+                                            opts ? opts->max_blocks : 0, opts ? opts->jit : 0));
     *out = s.release();
     return QI_OK;
   });
@@ -352,6 +356,8 @@ int qi_search_step(qi_search* s, qi_step_info* info) {
       info->blocks = si.blocks;
       info->new_witnesses = si.new_witnesses;
       info->kernel_ms = si.kernel_ms;
+      info->specialized = si.specialized ? 1u : 0u;
+      info->pad = 0;
     }
     return QI_OK;
   });
@@ -430,6 +436,24 @@ int qi_search_restart(qi_search* s) {
 }
 
 double qi_search_kernel_ms(const qi_search* s) { return s ? s->sd->sum_kernel_ms() : 0.0; }
+
+int qi_search_wait_jit(qi_search* s) {
+  if (!s) return fail(QI_ERR_ARG, "null");
+  return s->sd->wait_jit() ? 1 : 0;
+}
+
+int qi_fbas_jit_precompile(qi_fbas* f, double* ms) {
+  if (!f) return fail(QI_ERR_ARG, "null");
+  return guarded([&] {
+    if (f->sccs.members.empty()) throw qi::Error(QI_ERR_STATE, "empty FBAS");
+    auto t0 = std::chrono::steady_clock::now();
+    qi::LocalFlat lf = qi::flatten_local(f->g, f->sccs.members.front());
+    std::string log;
+    if (!qi::jit_precompile(lf, &log)) throw qi::Error(QI_ERR_UNSUPPORTED, "jit: " + log);
+    if (ms) *ms = ms_since(t0);
+    return QI_OK;
+  });
+}
 
 int qi_search_shape(const qi_search* s, qi_shape* out) {
   if (!s || !out) return fail(QI_ERR_ARG, "null");

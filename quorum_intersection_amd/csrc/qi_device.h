@@ -35,6 +35,11 @@ struct SearchConfig {
   uint32_t grace = 64;           // per-lane steps after the unit queue runs dry
   uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output)
   bool keep_log = true;          // keep per-segment records for preorder-exact counts
+  // Run-time specialised kernel (qi_jit.cpp): 0 = auto (compile in the background once a
+  // search reaches `jit_after` launches, switch at the next launch boundary), 1 = off
+  // (table-interpreting kernel only), 2 = sync (compile before the first launch).
+  uint32_t jit = 0;
+  uint32_t jit_after = 3;
 };
 
 struct StepInfo {
@@ -44,6 +49,7 @@ struct StepInfo {
   uint64_t new_witnesses = 0;
   double kernel_ms = 0;          // HIP-event time of the search kernel
   bool has_best = false;
+  bool specialized = false;      // launched the run-time specialised kernel
 };
 
 struct Totals {
@@ -82,8 +88,13 @@ class SearchDevice {
   virtual void drop_log() = 0;                      // forget processed segments
   virtual double sum_kernel_ms() const = 0;
   virtual uint64_t launches() const = 0;
+  virtual uint64_t specialized_launches() const = 0;
+  virtual bool wait_jit() = 0;                      // finish a pending compile; true if loaded
 };
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg);
+
+// hipRTC-compile the specialised kernel for this SCC's template shape (no GPU needed).
+bool jit_precompile(const LocalFlat& f, std::string* log);
 
 int device_count();
 int device_cu_count(int device);

@@ -1,0 +1,206 @@
+// Run-time specialisation of the search kernel (hipRTC).
+//
+// The search spends its time in containsQuorum (cpp:140-177) and findBestNode
+// (cpp:203-250) over ONE flattened SCC.  The ahead-of-time kernel interprets the packed
+// threshold-node table (scalar loads, loop control, flag tests per node: ~80% of the
+// issued instructions in profile r01b).  Here the same kernel source
+// (qi_search_kernel.h) is compiled once more with an evaluator generated for the given
+// SCC: every threshold node becomes v_and_b32 + v_bcnt_u32_b32 on literal masks and a
+// compare with a literal threshold, fully unrolled.  Code objects are cached on disk by
+// a hash of their source.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "qi_jit.h"
+#include "../../include/quorum_intersection.h"
+
+#include "qi_search_kernel_src.inc"  // kSearchKernelSrc: qi_search_kernel.h as a string
+
+namespace qi {
+namespace {
+
+std::string hex(uint32_t v) {
+  char b[16];
+  std::snprintf(b, sizeof b, "0x%08xu", v);
+  return b;
+}
+
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+std::string cache_dir() {
+  if (const char* e = std::getenv("QI_JIT_CACHE")) return e;
+  Dl_info info;
+  if (dladdr((void*)&fnv1a, &info) && info.dli_fname) {
+    std::string p = info.dli_fname;
+    auto k = p.rfind('/');
+    if (k != std::string::npos) return p.substr(0, k) + "/jit_cache";
+  }
+  return "/tmp/qi_jit_cache";
+}
+
+}  // namespace
+
+bool jit_eligible(const LocalFlat& f) {
+  return f.T <= 1024 && f.G <= 1024 && f.extra_src.size() <= 4096 && f.grp_extra.size() <= 4096 * 8;
+}
+
+std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX) {
+  std::ostringstream o;
+  o << kSearchKernelSrc << "\nnamespace qi {\nnamespace dev {\n";
+  o << "// generated evaluator: m=" << f.m << " T=" << f.T << " R=" << f.R << " G=" << f.G << "\n";
+  o << "struct SpecEval {\n";
+  // ---------------- containsQuorum ----------------
+  o << "  template <int POL>\n  static __device__ __forceinline__ bool gfp(const LocalDev&, uint32_t (&X)[" << MW
+    << "], uint32_t pol, uint32_t& rounds) {\n    (void)pol;\n    for (;;) {\n      if (!(X[0]";
+  for (int w = 1; w < MW; ++w) o << " | X[" << w << "]";
+  o << ")) return false;\n      ++rounds;\n";
+  for (int w = 0; w < TW; ++w) o << "      uint32_t sb" << w << " = 0u;\n";
+  std::vector<std::vector<std::string>> extra(f.T);
+  for (uint32_t t = 0; t < f.T; ++t)
+    for (uint32_t e = f.extra_off[t]; e < f.extra_off[t + 1]; ++e) {
+      const uint32_t src = f.extra_src[e];
+      const std::string m = hex(f.extra_mask[e]);
+      if (src < f.mw) extra[t].push_back("__popc(X[" + std::to_string(src) + "] & " + m + ")");
+      else extra[t].push_back("__popc(sb" + std::to_string(src - f.mw) + " & " + m + ")");
+    }
+  for (uint32_t t = 0; t < f.T; ++t) {
+    std::vector<std::string> terms;
+    for (uint32_t w = 0; w < f.mw; ++w) {
+      const uint32_t m = f.vmask[(size_t)t * f.mw + w];
+      if (m) terms.push_back("__popc(X[" + std::to_string(w) + "] & " + hex(m) + ")");
+    }
+    for (uint32_t w = 0; w < f.tw; ++w) {
+      const uint32_t m = f.cmask[(size_t)t * f.tw + w];
+      if (m) terms.push_back("__popc(sb" + std::to_string(w) + " & " + hex(m) + ")");
+    }
+    for (auto& x : extra[t]) terms.push_back(x);
+    std::string c = terms.empty() ? std::string("0u") : terms[0];
+    for (size_t i = 1; i < terms.size(); ++i) c += " + " + terms[i];
+    const bool inv = (f.flags[t] & 1u) != 0;
+    const int32_t t0 = f.thr[2 * t], t1 = f.thr[2 * t + 1];
+    std::string bit;
+    if (inv) {
+      bit = "(c == 0u)";
+    } else {
+      auto cmp = [&](int32_t th) -> std::string {
+        if (th <= 0) return "true";
+        if (th == INT32_MAX) return "false";
+        return "(c >= " + std::to_string(th) + "u)";
+      };
+      if (t0 == t1) bit = cmp(t0);
+      else bit = "(POL == 0 ? " + cmp(t0) + " : POL == 1 ? " + cmp(t1) + " : (pol ? " + cmp(t1) + " : " + cmp(t0) + "))";
+    }
+    o << "      { const uint32_t c = " << c << "; (void)c; sb" << (t / 32) << " |= (uint32_t)(" << bit << ") << "
+      << (t % 32) << "u; }\n";
+  }
+  for (int w = 0; w < MW; ++w) o << "      uint32_t n" << w << " = 0u;\n";
+  for (uint32_t r = 0; r < f.R; ++r) {
+    const uint32_t tn = f.root_tn[r];
+    o << "      { const uint32_t s = 0u - ((sb" << (tn / 32) << " >> " << (tn % 32) << "u) & 1u);";
+    for (uint32_t w = 0; w < f.mw; ++w) {
+      const uint32_t u = f.root_users[(size_t)r * f.mw + w];
+      if (u) o << " n" << w << " |= " << hex(u) << " & s;";
+    }
+    o << " }\n";
+  }
+  o << "      bool same = true;\n";
+  for (int w = 0; w < MW; ++w) o << "      n" << w << " &= X[" << w << "]; same &= (n" << w << " == X[" << w << "]);\n";
+  o << "      if (same) return true;\n";
+  for (int w = 0; w < MW; ++w) o << "      X[" << w << "] = n" << w << ";\n";
+  o << "    }\n  }\n";
+  // ---------------- findBestNode ----------------
+  o << "  static __device__ __forceinline__ uint32_t best(const LocalDev&, const uint32_t (&Q)[" << MW
+    << "], const uint32_t (&D)[" << MW << "], uint32_t& zero_fallback) {\n"
+    << "    uint32_t bestdeg = 0u, bestv = 0xFFFFFFFFu;\n";
+  for (uint32_t g = 0; g < f.G; ++g) {
+    std::vector<std::string> terms;
+    for (uint32_t w = 0; w < f.mw; ++w) {
+      const uint32_t m = f.grp_col[(size_t)g * f.mw + w];
+      if (m) terms.push_back("__popc(Q[" + std::to_string(w) + "] & " + hex(m) + ")");
+    }
+    for (uint32_t e = f.grp_extra_off[g]; e < f.grp_extra_off[g + 1]; ++e)
+      for (uint32_t w = 0; w < f.mw; ++w) {
+        const uint32_t m = f.grp_extra[(size_t)e * f.mw + w];
+        if (m) terms.push_back("__popc(Q[" + std::to_string(w) + "] & " + hex(m) + ")");
+      }
+    std::string deg = terms.empty() ? std::string("0u") : terms[0];
+    for (size_t i = 1; i < terms.size(); ++i) deg += " + " + terms[i];
+    o << "    { const uint32_t deg = " << deg << "; uint32_t low = 0xFFFFFFFFu;";
+    for (int w = (int)f.mw - 1; w >= 0; --w) {
+      const uint32_t m = f.grp_members[(size_t)g * f.mw + w];
+      if (!m) continue;
+      o << " { const uint32_t c = Q[" << w << "] & ~D[" << w << "] & " << hex(m) << "; low = c ? " << (w * 32)
+        << "u + (uint32_t)__builtin_ctz(c) : low; }";
+    }
+    o << "\n      const bool better = (low != 0xFFFFFFFFu) && (deg > bestdeg || (deg == bestdeg && low < bestv));"
+      << " bestdeg = better ? deg : bestdeg; bestv = better ? low : bestv; }\n";
+  }
+  o << "    zero_fallback += (bestdeg == 0u) ? 1u : 0u;\n    return bestv;\n  }\n};\n";
+  o << "}  // namespace dev\n}  // namespace qi\n\n";
+  o << "extern \"C\" __global__ __launch_bounds__(64) void qi_search_spec(qi::dev::SearchArgs a) {\n"
+    << "  qi::dev::search_body<" << MW << ", " << TW << ", " << SMAX << ", qi::dev::SpecEval>(a);\n}\n";
+  return o.str();
+}
+
+std::vector<char> jit_compile(const std::string& src, std::string* log) {
+  const std::string dir = cache_dir();
+  char key[32];
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v1"));
+  const std::string path = dir + "/" + key + ".co";
+  {
+    std::ifstream in(path, std::ios::binary);
+    if (in) {
+      std::vector<char> code((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+      if (!code.empty()) return code;
+    }
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "qi_search_spec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    if (log) *log = "hiprtcCreateProgram failed";
+    return {};
+  }
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pragma-once-outside-header"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+  size_t n = 0;
+  hiprtcGetProgramLogSize(prog, &n);
+  std::string lg(n, '\0');
+  if (n) hiprtcGetProgramLog(prog, &lg[0]);
+  if (log) *log = lg;
+  std::vector<char> code;
+  if (rc == HIPRTC_SUCCESS) {
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    code.resize(cs);
+    hiprtcGetCode(prog, code.data());
+    ::mkdir(dir.c_str(), 0755);
+    const std::string tmp = path + ".tmp" + std::to_string(::getpid());
+    {
+      std::ofstream out(tmp, std::ios::binary);
+      out.write(code.data(), (std::streamsize)code.size());
+    }
+    std::rename(tmp.c_str(), path.c_str());
+  }
+  hiprtcDestroyProgram(&prog);
+  return code;
+}
+
+}  // namespace qi

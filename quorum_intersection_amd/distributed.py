@@ -54,13 +54,13 @@ class SearchBackend:
 class DeviceSearch(SearchBackend):
     """C-ABI step-wise search (include/quorum_intersection.h) on one HIP device."""
 
-    def __init__(self, fbas, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0):
+    def __init__(self, fbas, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0, jit: int = 0):
         from . import _capi
         self._c = _capi
         self.L = _capi.lib()
         self.fbas = fbas
         h = ctypes.c_void_p()
-        opts = _capi.SearchOpts(grow_budget, run_budget, max_blocks)
+        opts = _capi.SearchOpts(grow_budget, run_budget, max_blocks, jit)
         _capi.check(self.L.qi_search_create(fbas.handle, ctypes.byref(opts), ctypes.byref(h)))
         self.h = h
         self.key_words = int(self.L.qi_search_key_words(h))
@@ -107,6 +107,7 @@ class DeviceSearch(SearchBackend):
         self._c.check(self.L.qi_search_step(self.h, ctypes.byref(info)))
         self.kernel_ms += info.kernel_ms
         self.launches += 1
+        self.spec_launches = getattr(self, "spec_launches", 0) + int(info.specialized)
 
     def frontier(self) -> int:
         return int(self.L.qi_search_frontier(self.h))
@@ -140,6 +141,9 @@ class DeviceSearch(SearchBackend):
             self._c.check(self.L.qi_search_reduce(self.h, k, key[1], ctypes.byref(t)))
         return {"nodes": t.nodes, "evals": t.evals, "minq": t.minq, "zero_fallback": t.zero_fallback,
                 "rounds": t.rounds, "units": t.units, "wave_iters": t.wave_iters, "coop_phases": t.coop_phases}
+
+    def wait_jit(self) -> bool:
+        return self.L.qi_search_wait_jit(self.h) == 1
 
     def shape(self) -> Dict[str, int]:
         sh = self._c.Shape()

@@ -36,7 +36,21 @@ def instances():
         yield f"random_{s}", random_fbas(s)
 
 
+def big():
+    """Bench-size instances (minutes of single-threaded oracle time each)."""
+    o = Oracle()
+    out = {}
+    for k in (9, 10):
+        r = o.load(fbas_gen.two_tier(k, 256)).solve()
+        out[f"two_tier_{k}_256"] = {"verdict": r["verdict"], "nodes": r["nodes"], "evals": r["evals"],
+                                    "minq": r["minq"], "nscc": r["nscc"], "oracle_seconds": round(r["seconds"], 2)}
+    with open(os.path.join(HERE, "golden_big.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
+    if "--big" in sys.argv:
+        return big()
     o = Oracle()
     out = {}
     for name, text in instances():

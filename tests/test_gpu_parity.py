@@ -104,10 +104,13 @@ def test_contains_quorum_api_order():
 
 
 # ---- solve(Graph): verdict, counts, witness --------------------------------------------
+@pytest.mark.parametrize("jit", [1, 2], ids=["table", "specialised"])
 @pytest.mark.parametrize("name", sorted(GOLD))
-def test_solve_matches_golden(name):
+def test_solve_matches_golden(name, jit):
     text = _text_for(name)
-    d = qa.FBAS(text).solve_stats()
+    d = qa.FBAS(text).solve_stats(jit=jit)
+    if jit == 2 and d["searched"] and d["launches"]:
+        assert d["jit_launches"] == d["launches"]
     _cmp(d, GOLD[name], name)
     if not d["verdict"] and d["searched"]:
         _validate_witness(text, d["q1"], d["q2"])
@@ -117,7 +120,7 @@ def test_solve_matches_golden(name):
 def test_solve_random_org(seed):
     text = random_org_fbas(seed, n_orgs=5 + seed % 4)
     r = Oracle().load(text).solve()
-    d = qa.FBAS(text).solve_stats()
+    d = qa.FBAS(text).solve_stats(jit=2 if seed % 2 else 1)
     _cmp(d, r, f"org{seed}")
     if not d["verdict"] and d["searched"]:
         _validate_witness(text, d["q1"], d["q2"])
@@ -128,18 +131,20 @@ def test_solve_tiny_budgets_exercise_the_frontier(cfg):
     # budgets of a few nodes per lane force many launches, spills, ring carry-overs and
     # (with one block) LDS-stack evictions; counts must not change
     grow, run, blocks = cfg
-    for name in ("tiered_4", "tiered_5", "broken", "correct", "planted_4_64", "tiered_5_shuffled"):
-        d = qa.FBAS(_text_for(name)).solve_stats(grow, run, blocks)
-        _cmp(d, GOLD[name], name)
-    for seed in (0, 4, 9, 12, 16, 17):
-        text = random_org_fbas(seed, n_orgs=5 + seed % 4)
-        _cmp(qa.FBAS(text).solve_stats(grow, run, blocks), Oracle().load(text).solve(), f"org{seed}")
+    for jit in (1, 2):
+        for name in ("tiered_4", "tiered_5", "broken", "correct", "planted_4_64", "tiered_5_shuffled"):
+            d = qa.FBAS(_text_for(name)).solve_stats(grow, run, blocks, jit)
+            _cmp(d, GOLD[name], name)
+        for seed in (0, 4, 9, 12, 16, 17):
+            text = random_org_fbas(seed, n_orgs=5 + seed % 4)
+            _cmp(qa.FBAS(text).solve_stats(grow, run, blocks, jit), Oracle().load(text).solve(), f"org{seed}")
 
 
 def test_solve_tiered_6_7_exact():
     for k in (6, 7):
-        d = qa.FBAS(fbas_gen.tiered(k)).solve_stats()
-        _cmp(d, GOLD[f"tiered_{k}"], k)
+        for jit in (1, 2):
+            d = qa.FBAS(fbas_gen.tiered(k)).solve_stats(jit=jit)
+            _cmp(d, GOLD[f"tiered_{k}"], k)
 
 
 def test_solve_two_tier_256():
@@ -149,8 +154,23 @@ def test_solve_two_tier_256():
 
 def test_tiered_8_full_search_counts():
     # 1,857,737 search calls, 3,030,461 fixpoint evals, 20,412 minimal quorums
-    d = qa.FBAS(fbas_gen.tiered(8)).solve_stats()
-    assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (True, 1857737, 3030461 + 0, 20412)
+    for jit in (0, 1, 2):
+        d = qa.FBAS(fbas_gen.tiered(8)).solve_stats(jit=jit)
+        assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (True, 1857737, 3030461 + 0, 20412)
+
+
+BIG = json.load(open(os.path.join(GOLDEN, "golden_big.json")))
+
+
+@pytest.mark.parametrize("name", sorted(BIG))
+def test_big_two_tier_counts(name):
+    # bench-size workloads; golden counts from the oracle's full CPU search
+    # (tests/golden/make_golden.py --big: ~70 s and ~450 s single-threaded)
+    _, _, k, n = name.split("_")
+    for jit in (1, 2):
+        d = qa.FBAS(fbas_gen.two_tier(int(k), int(n))).solve_stats(jit=jit)
+        g = BIG[name]
+        assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (g["verdict"], g["nodes"], g["evals"], g["minq"])
 
 
 def test_large_scc_multiword_masks():
@@ -160,8 +180,9 @@ def test_large_scc_multiword_masks():
         text = fbas_gen.planted(k, n)
         r = Oracle().load(text).solve()
         assert len(r["front"]) > 32
-        d = qa.FBAS(text).solve_stats()
-        _cmp(d, r, f"planted_{k}_{n}")
+        for jit in (1, 2):
+            d = qa.FBAS(text).solve_stats(jit=jit)
+            _cmp(d, r, f"planted_{k}_{n}")
         if not d["verdict"]:
             _validate_witness(text, d["q1"], d["q2"])
 
@@ -206,7 +227,7 @@ def _two_way_search(text, hand_every=1, move_frac=0.5):
     L = _capi.lib()
     fa, fb = qa.FBAS(text), qa.FBAS(text)
     sa, sb = ctypes.c_void_p(), ctypes.c_void_p()
-    opts = _capi.SearchOpts(2, 8, 2)
+    opts = _capi.SearchOpts(2, 8, 2, 2)
     _capi.check(L.qi_search_create(fa.handle, ctypes.byref(opts), ctypes.byref(sa)))
     _capi.check(L.qi_search_create(fb.handle, ctypes.byref(opts), ctypes.byref(sb)))
     _capi.check(L.qi_search_clear(sb))

@@ -148,3 +148,19 @@ def test_cli_help_and_invalid_option():
     r = subprocess.run([exe, "-p"], input=fixture_text("correct_trivial"), capture_output=True)
     assert r.returncode == 0
     assert r.stdout.decode() == Oracle().load(fixture_text("correct_trivial")).pagerank_text()
+
+
+@pytest.mark.parametrize("case", ["broken", "two_tier_10", "planted_20_80", "org_multiplicity", "threshold0"])
+def test_specialised_kernel_sources_compile(case):
+    # hipRTC compiles the generated evaluator + the shared kernel header for gfx950 on the
+    # CPU (no device needed); exercised at run time by the -m gpu parity suite.
+    from qi_testlib import random_org_fbas
+    texts = {
+        "broken": fixture_text("broken"),
+        "two_tier_10": fbas_gen.two_tier(10, 256),
+        "planted_20_80": fbas_gen.planted(20, 80),
+        "org_multiplicity": random_org_fbas(9, 7),
+        "threshold0": random_org_fbas(3, 6, t0=True),
+    }
+    ms = qa.FBAS(texts[case]).jit_precompile()
+    assert ms >= 0
