@@ -19,7 +19,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "search_kernel"
+KERNEL = "qi_search_spec"  # run-time specialised search kernel (bench default)
 
 
 def agg_counters(path):
@@ -56,16 +56,16 @@ def main():
         tot, disp = agg_counters(f)
         for (k, c), v in tot.items():
             counters.setdefault(k, {})[c] = v
-            if KERNEL in k:
+            if KERNEL in k or ("search_kernel" in k and not any(KERNEL in kk for kk, _ in tot)):
                 per_dispatch[c] = v / max(len(disp[(k, c)]), 1)
-    search = [s for s in stats if KERNEL in s["Name"]][0]
+    search = ([s for s in stats if KERNEL in s["Name"]] or [s for s in stats if "search_kernel" in s["Name"]])[0]
     out = {"kernel_stats_search": search, "search_kernel_per_dispatch": per_dispatch, "totals": counters}
     json.dump(out, open(os.path.join(dst, "counters.json"), "w"), indent=1)
     pdc = per_dispatch
     lines = [f"# Profile {a.tag}", "", a.note, "",
              "`tools/profile.sh` on one MI355X: `rocprofv3 --kernel-trace --stats` + separate `--pmc` passes "
              "(bench.py default workload two_tier(k_top=10, 256)).", "",
-             "## Kernel stats (search_kernel)", "",
+             f"## Kernel stats ({search['Name'][:60]})", "",
              f"- calls {search['Calls']}, average {float(search['AverageNs'])/1e3:.1f} us, "
              f"min {float(search['MinNs'])/1e3:.1f} us, max {float(search['MaxNs'])/1e3:.1f} us, "
              f"{float(search['Percentage']):.1f}% of GPU time", "",
