@@ -84,7 +84,8 @@ typedef struct {
   uint32_t run_budget;     /* 0 = default: per-lane node budget at full occupancy */
   uint32_t max_blocks;     /* 0 = default (8 wavefronts per CU) */
   uint32_t jit;            /* run-time specialised search kernel: 0 auto (background compile
-                              once a search needs >= 3 launches), 1 off, 2 before launch 1 */
+                              once a search needs >= 3 launches), 1 off, 2 before launch 1,
+                              3 = 2 + diagnostic section stamps (not for measurement) */
 } qi_solve_opts;
 
 typedef struct {
@@ -151,6 +152,7 @@ typedef struct {
   uint64_t units;        /* frontier units fetched (all launches) */
   uint64_t wave_iters;   /* search-loop iterations summed over wavefronts */
   uint64_t coop_phases;  /* iterations that ran the cooperative minimality phase */
+  uint64_t stamps[8];    /* jit = 3 diagnostic build: s_memtime cycles per loop section */
 } qi_totals;
 
 /* Shape of the flattened searched SCC (for work accounting). */

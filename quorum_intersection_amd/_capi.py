@@ -83,7 +83,8 @@ class Shape(ctypes.Structure):
 
 class Totals(ctypes.Structure):
     _fields_ = [("nodes", c_uint64), ("evals", c_uint64), ("minq", c_uint64), ("zero_fallback", c_uint64),
-                ("rounds", c_uint64), ("units", c_uint64), ("wave_iters", c_uint64), ("coop_phases", c_uint64)]
+                ("rounds", c_uint64), ("units", c_uint64), ("wave_iters", c_uint64), ("coop_phases", c_uint64),
+                ("stamps", c_uint64 * 8)]
 
 
 # name -> (restype, argtypes); must match include/quorum_intersection.h exactly

@@ -410,6 +410,7 @@ int qi_search_reduce(qi_search* s, const uint32_t* key, uint32_t depth, qi_total
     out->units = t.units;
     out->wave_iters = t.wave_iters;
     out->coop_phases = t.coop_phases;
+    for (int q = 0; q < 8; ++q) out->stamps[q] = t.dbg[q];
     return QI_OK;
   });
 }

@@ -37,7 +37,8 @@ struct SearchConfig {
   bool keep_log = true;          // keep per-segment records for preorder-exact counts
   // Run-time specialised kernel (qi_jit.cpp): 0 = auto (compile in the background once a
   // search reaches `jit_after` launches, switch at the next launch boundary), 1 = off
-  // (table-interpreting kernel only), 2 = sync (compile before the first launch).
+  // (table-interpreting kernel only), 2 = sync (compile before the first launch),
+  // 3 = sync diagnostic build with s_memtime section stamps (never for measurements).
   uint32_t jit = 0;
   uint32_t jit_after = 3;
 };
@@ -55,6 +56,7 @@ struct StepInfo {
 struct Totals {
   uint64_t nodes = 0, evals = 0, minq = 0, zero_fallback = 0, rounds = 0;
   uint64_t units = 0, wave_iters = 0, coop_phases = 0;  // occupancy accounting (unfiltered)
+  uint64_t dbg[8] = {0, 0, 0, 0, 0, 0, 0, 0};           // diagnostic stamps (jit = 3)
 };
 
 struct Witness {

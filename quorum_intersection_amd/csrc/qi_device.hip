@@ -379,24 +379,30 @@ class SearchDeviceImpl : public SearchDevice {
     for (uint32_t w = 0; w < 8; ++w) scc_mask_[w] = 0;
     for (uint32_t v = 0; v < f.m; ++v) scc_mask_[v >> 5] |= 1u << (v & 31);
 
-    int cus = device_cu_count(device_);
-    max_blocks_ = cfg_.max_blocks ? cfg_.max_blocks : (uint32_t)cus * 8u;
+    cus_ = (uint32_t)device_cu_count(device_);
+    max_blocks_ = cfg_.max_blocks ? cfg_.max_blocks : cus_ * 8u;  // refined below once shm_ is known
     counters_ = dalloc<uint32_t>(4);
-    totals_ = dalloc<unsigned long long>(8);
+    totals_ = dalloc<unsigned long long>(16);
     best64_ = dalloc<unsigned long long>(1);
     red_ = dalloc<unsigned long long>(4);
     keydev_ = dalloc<uint32_t>(8);
     wit_cap_ = 1u << 16;
     wit_ = dalloc<uint32_t>((size_t)wit_cap_ * WL::WORDS);
-    HIP_CHECK(hipMemsetAsync(totals_, 0, 8 * sizeof(unsigned long long), stream_));
+    HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * sizeof(unsigned long long), stream_));
     unsigned long long inf = ~0ull;
     HIP_CHECK(hipMemcpyAsync(best64_, &inf, 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
-    shm_ = (size_t)(SMAX * (MW + 1) * 64 + 3 * MW * 64 + 68 + UL::WORDS * 64) * 4 + (size_t)UL::DMAX * 64;
+    shm_ = (size_t)(SMAX * (MW + 1) * 64 + 2 * MW * 64 + UL::WORDS * 64 + ((UL::DMAX + 3) / 4) * 64) * 4;
     shm_ = (shm_ + 15) / 16 * 16;
     HIP_CHECK(hipFuncSetAttribute((const void*)dev::search_kernel<MW, TW, SMAX>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
-    if (cfg_.jit == 2 && jit_eligible(flat_)) {
+    if (!cfg_.max_blocks) {  // one resident wave of blocks: no second-wave tail
+      int nb = 0;
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)dev::search_kernel<MW, TW, SMAX>, 64,
+                                                             shm_));
+      if (nb > 0) max_blocks_ = cus_ * (uint32_t)nb;
+    }
+    if ((cfg_.jit == 2 || cfg_.jit == 3) && jit_eligible(flat_)) {
       start_jit();
       if (!wait_jit()) throw Error(QI_ERR_UNSUPPORTED, "specialised kernel failed to build: " + jit_log_);
     }
@@ -470,6 +476,15 @@ class SearchDeviceImpl : public SearchDevice {
     a.grace = cfg_.grace;
     a.evict_max = cfg_.evict_max;
     a.half_m = m_ / 2;
+    {  // cooperative slot: smallest power of two covering |D| + 1 <= half_m + 1 jobs
+      uint32_t sl = 1, lg = 0;
+      while (sl < a.half_m + 1 && sl < 64) {
+        sl <<= 1;
+        ++lg;
+      }
+      a.coop_slot = sl;
+      a.coop_slot_log2 = lg;
+    }
     a.has_best = has_best_ ? 1u : 0u;
     a.best_depth = best_depth_;
     for (int w = 0; w < 8; ++w) {
@@ -607,12 +622,13 @@ class SearchDeviceImpl : public SearchDevice {
     t.units = rt.units;
     t.wave_iters = rt.wave_iters;
     t.coop_phases = rt.coop_phases;
+    for (int q = 0; q < 8; ++q) t.dbg[q] = rt.dbg[q];
     return t;
   }
 
   Totals running_totals() const override {
     DeviceGuard dg(device_);
-    unsigned long long r[8];
+    unsigned long long r[16];
     HIP_CHECK(hipMemcpyAsync(r, totals_, sizeof r, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
     Totals t;
@@ -624,13 +640,14 @@ class SearchDeviceImpl : public SearchDevice {
     t.units = r[5];
     t.wave_iters = r[6];
     t.coop_phases = r[7];
+    for (int q = 0; q < 8; ++q) t.dbg[q] = r[8 + q];
     return t;
   }
 
   void drop_log() override {
     for (auto& c : log_) c.used = 0;
     DeviceGuard dg(device_);
-    HIP_CHECK(hipMemsetAsync(totals_, 0, 8 * sizeof(unsigned long long), stream_));
+    HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * sizeof(unsigned long long), stream_));
     unsigned long long inf = ~0ull;
     HIP_CHECK(hipMemcpyAsync(best64_, &inf, 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -717,6 +734,7 @@ class SearchDeviceImpl : public SearchDevice {
   std::vector<void*> bufs_;
   uint32_t scc_mask_[8];
   uint32_t max_blocks_ = 0;
+  uint32_t cus_ = 0;
   uint32_t* units_[2] = {nullptr, nullptr};
   uint64_t cap_[2] = {0, 0};
   int cur_ = 0;
@@ -749,7 +767,7 @@ class SearchDeviceImpl : public SearchDevice {
 
   void start_jit() {
     jit_state_.store(1);
-    std::string src = jit_source(flat_, MW, TW, SMAX);
+    std::string src = jit_source(flat_, MW, TW, SMAX, cfg_.jit == 3);
     jit_thread_ = std::thread([this, src]() {
       std::vector<char> code = jit_compile(src, &jit_log_);
       jit_code_ = std::move(code);
@@ -768,6 +786,11 @@ class SearchDeviceImpl : public SearchDevice {
       return;
     }
     jit_state_.store(4);
+    if (!cfg_.max_blocks) {
+      int nb = 0;
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jit_fn_, 64, shm_) == hipSuccess && nb > 0)
+        max_blocks_ = cus_ * (uint32_t)nb;
+    }
   }
 };
 

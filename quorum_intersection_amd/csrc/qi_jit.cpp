@@ -63,8 +63,9 @@ bool jit_eligible(const LocalFlat& f) {
   return f.T <= 1024 && f.G <= 1024 && f.extra_src.size() <= 4096 && f.grp_extra.size() <= 4096 * 8;
 }
 
-std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX) {
+std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps) {
   std::ostringstream o;
+  if (stamps) o << "#define QI_STAMPS 1\n";
   o << kSearchKernelSrc << "\nnamespace qi {\nnamespace dev {\n";
   o << "// generated evaluator: m=" << f.m << " T=" << f.T << " R=" << f.R << " G=" << f.G << "\n";
   o << "struct SpecEval {\n";

@@ -11,7 +11,7 @@ namespace qi {
 // Whether a generated evaluator stays a reasonable size for this SCC.
 bool jit_eligible(const LocalFlat& f);
 // Full hipRTC source: qi_search_kernel.h + generated SpecEval + extern "C" qi_search_spec.
-std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX);
+std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps = false);
 // Compile for gfx950 (or read the on-disk cache); empty on failure, log in *log.
 std::vector<char> jit_compile(const std::string& src, std::string* log);
 

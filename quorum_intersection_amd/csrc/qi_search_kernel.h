@@ -231,6 +231,8 @@ struct SearchArgs {
   uint32_t grace;                // extra steps per lane once the unit queue is dry
   uint32_t evict_max;
   uint32_t half_m;
+  uint32_t coop_slot;            // lanes per pending owner in the cooperative phase (pow2)
+  uint32_t coop_slot_log2;
   uint32_t has_best;             // host-known best key (multiword) for pruning
   uint32_t best_depth;
   uint32_t best_key[8];
@@ -281,6 +283,24 @@ __device__ __forceinline__ uint32_t reserve(uint32_t n, uint32_t* counter, uint3
   return base + x - n;
 }
 
+// Diagnostic build only (QI_STAMPS, run-time specialised kernel with jit=3): per-wave
+// s_memtime sums of the loop sections, added into totals[8..15].  The production kernels
+// contain no stamps (MI355X guide §7 "In-kernel stamps": read shares, not lengths).
+#ifdef QI_STAMPS
+#define QI_STAMP(slot)                                                   \
+  do {                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();                  \
+    __builtin_amdgcn_sched_barrier(0);                                   \
+    stamp_sum[(slot)] += now_ - stamp_prev;                              \
+    stamp_prev = now_;                                                   \
+  } while (0)
+#else
+#define QI_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
+
 template <int MW, int TW, int SMAX, class EV>
 __device__ __forceinline__ void search_body(const SearchArgs& a) {
   using UL = UnitLayout<MW>;
@@ -290,20 +310,23 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   constexpr int UW = UL::WORDS;
   constexpr int SE = MW + 1;  // stack entry words: T'[MW], packed(b, depth, dlen)
 
+  constexpr int OW = (DMAX + 3) / 4;  // packed D-order words (4 vertex bytes each)
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* st = lds;                                          // [SMAX][SE][64]
-  uint32_t* co_D = st + SMAX * SE * WAVE;                       // [MW][64]
-  uint32_t* co_NE = co_D + MW * WAVE;                           // [MW][64]
-  uint32_t* co_VIS = co_NE + MW * WAVE;                         // [MW][64]
-  uint32_t* co_off = co_VIS + MW * WAVE;                        // [65] (+pad)
-  uint32_t* uring = co_off + 68;                                // [UW][64] staged units
-  uint8_t* dord = (uint8_t*)(uring + UW * WAVE);                // [DMAX][64]
+  uint32_t* co_NE = st + SMAX * SE * WAVE;                      // [MW][64] per pending rank
+  uint32_t* co_VIS = co_NE + MW * WAVE;                         // [MW][64] per pending rank
+  uint32_t* uring = co_VIS + MW * WAVE;                         // [UW][64] staged units
+  uint32_t* dow = uring + UW * WAVE;                            // [OW][64] D in branch order
 
   const uint32_t lane = threadIdx.x;
   const LocalDev& f = a.f;
 #define ST_(lvl, w) st[((lvl) * SE + (w)) * WAVE + lane]
-#define DO_(i) dord[(i) * WAVE + lane]
+#define DOW_(w) dow[(w) * WAVE + lane]
 #define UR_(w, slot) uring[(w) * WAVE + (slot)]
+  // byte i of this lane's D order (ds_write_b8 into the packed word)
+  auto set_ord = [&](uint32_t i, uint32_t v) {
+    ((uint8_t*)dow)[(((i >> 2) * WAVE + lane) << 2) + (i & 3u)] = (uint8_t)v;
+  };
 
   uint32_t T[MW], D[MW], K[MW];
 #pragma unroll
@@ -324,6 +347,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint64_t tot_nodes = 0, tot_evals = 0, tot_minq = 0, tot_zfb = 0, tot_fetched = 0;
   uint32_t rounds = 0;
   uint32_t wave_iters = 0, coop_phases = 0;  // wave-uniform: occupancy accounting
+#ifdef QI_STAMPS
+  uint64_t stamp_sum[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
+#endif
 
   // wave-uniform LDS ring of staged units (see (2) below)
   uint32_t ring_src = 0, ring_cnt = 0, ring_next = 0;
@@ -391,15 +418,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     const uint32_t ulen = ol + (extra_b >= 0 ? 1u : 0u);
     u[UL::DEPTH] = udepth;
     u[UL::DLEN] = ulen;
-    for (uint32_t i = 0; i < (uint32_t)(DMAX + 3) / 4; ++i) {
-      uint32_t word = 0;
-#pragma unroll
-      for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t p = i * 4 + j;
-        uint32_t byte = 0;
-        if (p < ol) byte = DO_(p);
-        else if (p == ol && extra_b >= 0) byte = (uint32_t)extra_b;
-        word |= byte << (8 * j);
+    for (uint32_t i = 0; i < (ulen + 3) / 4; ++i) {  // bytes >= ulen are don't-care
+      uint32_t word = DOW_(i);
+      if (extra_b >= 0 && i == (ol >> 2)) {
+        const uint32_t sh = 8u * (ol & 3u);
+        word = (word & ~(0xFFu << sh)) | ((uint32_t)extra_b << sh);
       }
       u[UL::ORD + i] = word;
     }
@@ -416,9 +439,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     }
     const uint32_t pk = ST_(pos, MW);
     const uint32_t b = pk & 255u, de = (pk >> 8) & 511u, dle = pk >> 17;
-    for (uint32_t i = 0; i < dle; ++i) {
-      const uint32_t v = DO_(i);
-      UD[v >> 5] |= 1u << (v & 31u);
+    for (uint32_t i = 0; i < (dle + 3) / 4; ++i) {
+      const uint32_t word = DOW_(i);
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j)
+        if (i * 4 + j < dle) {
+          const uint32_t v = (word >> (8 * j)) & 255u;
+          UD[v >> 5] |= 1u << (v & 31u);
+        }
     }
     UD[b >> 5] |= 1u << (b & 31u);
     key_prefix_bit<MW>(UK, de);
@@ -441,12 +469,19 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           nst = 0;
           break;
         }
-        for (uint32_t i = dle; i < dlen; ++i) {
-          const uint32_t v = DO_(i);
-          D[v >> 5] &= ~(1u << (v & 31u));
+        for (uint32_t i = dle >> 2; i < (dlen + 3) / 4; ++i) {  // drop inclusions below `de`
+          const uint32_t word = DOW_(i);
+#pragma unroll
+          for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t p = i * 4 + j;
+            if (p >= dle && p < dlen) {
+              const uint32_t v = (word >> (8 * j)) & 255u;
+              D[v >> 5] &= ~(1u << (v & 31u));
+            }
+          }
         }
         D[b >> 5] |= 1u << (b & 31u);
-        DO_(dle) = (uint8_t)b;
+        set_ord(dle, b);
         dlen = dle + 1;
 #pragma unroll
         for (int w = 0; w < MW; ++w) {
@@ -463,6 +498,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
+    QI_STAMP(0);  // pop / segment close
     // ---- (2) fetch new units from the wave's LDS ring --------------------------------
     // The ring holds up to 64 units staged by one coalesced refill (one atomic on the
     // global head + one unit per lane), so the global-load latency is paid once per 64
@@ -494,12 +530,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
         const uint32_t ud = UR_(UL::DEPTH, slot);
         dlen = UR_(UL::DLEN, slot);
-        for (uint32_t i = 0; i < (dlen + 3) / 4; ++i) {
-          const uint32_t word = UR_(UL::ORD + i, slot);
-#pragma unroll
-          for (uint32_t j = 0; j < 4; ++j)
-            if (i * 4 + j < dlen) DO_(i * 4 + j) = (uint8_t)(word >> (8 * j));
-        }
+        for (uint32_t i = 0; i < (dlen + 3) / 4; ++i) DOW_(i) = UR_(UL::ORD + i, slot);
         ++tot_fetched;
         seg_idx = ring_src + slot;
         seg_open = true;
@@ -539,6 +570,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
+    QI_STAMP(1);  // fetch + polls
     // ---- (3) budget exhausted: spill current node + stack to the next frontier --------
     {
       const bool spill = has && (steps >= limit || evictions >= a.evict_max);
@@ -557,6 +589,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
+    QI_STAMP(2);  // spill
     // ---- (4) one search node per active lane (cpp:258-345) ---------------------------
     ++wave_iters;
     bool pending = false;
@@ -584,6 +617,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = active2 ? (T[w] | D[w]) : 0u;
     const bool qne = EV::template gfp<0>(f, X, 0u, rounds);  // cpp:301
+    QI_STAMP(3);  // the two fixpoints
     bool push = false;
     uint32_t pb = 0;
     if (active2) {
@@ -631,80 +665,75 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
+    QI_STAMP(4);  // findBestNode + push
     // ---- (5) quorum leaves: isMinimalQuorum + visitor, wave-cooperative --------------
+    // Every pending lane (GFP(D) != ∅, cpp:281) needs |D| single-removal fixpoints
+    // (isMinimalQuorum, cpp:188-198) and the complement check of the visitor (cpp:368).
+    // Done per lane they would serialise the wave (the first removable vertex sits at a
+    // ~uniform position of the D order), so they are spread over the wave in fixed slots
+    // of S = a.coop_slot lanes per pending lane: lane l serves owner (l / S) of the
+    // current pass, job k = l % S (+ chunk offset when |D|+1 > S).  The owner's D arrives
+    // by __shfl, results by one LDS ds_or per successful job; one barrier per pass.
     const uint64_t pm = __ballot(pending);
     if (pm) {
       ++coop_phases;
       const uint32_t npend = (uint32_t)__popcll(pm);
       const uint32_t r = rank_in(pm);
-      uint32_t nj = pending ? dlen + 1u : 0u;
-      uint32_t x = nj;
-#pragma unroll
-      for (int d = 1; d < WAVE; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        if ((int)lane >= d) x += y;
-      }
-      const uint32_t J = __shfl(x, WAVE - 1);
+      const uint32_t S = a.coop_slot, lgS = a.coop_slot_log2;
+      const uint32_t P = (uint32_t)WAVE >> lgS;  // owners per pass
       if (pending) {
-        co_off[r] = x - nj;
 #pragma unroll
         for (int w = 0; w < MW; ++w) {
-          co_D[w * WAVE + r] = D[w];
           co_NE[w * WAVE + r] = 0u;
           co_VIS[w * WAVE + r] = 0u;
         }
       }
-      if (lane == 0) co_off[npend] = J;
       __syncthreads();
-      for (uint32_t j0 = 0; j0 < J; j0 += WAVE) {
-        const uint32_t j = j0 + lane;
-        const bool act = j < J;
-        uint32_t lo = 0;
-        if (act) {
-          uint32_t hi = npend - 1;
-          while (lo < hi) {  // last owner with co_off[o] <= j
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (co_off[mid] <= j) lo = mid;
-            else hi = mid - 1;
-          }
-        }
-        const uint32_t o = lo;
+      for (uint32_t q0 = 0; q0 < npend; q0 += P) {
+        const uint32_t oi = q0 + (lane >> lgS);
+        uint64_t mm = pm;
+        for (uint32_t c = 0; c < oi && mm; ++c) mm &= mm - 1ull;  // oi-th pending lane
+        const uint32_t ol = mm ? (uint32_t)__builtin_ctzll(mm) : 0u;
         uint32_t Dr[MW];
 #pragma unroll
-        for (int w = 0; w < MW; ++w) Dr[w] = act ? co_D[w * WAVE + o] : 0u;
-        const uint32_t k = act ? j - co_off[o] : 0u;
-        const uint32_t dl = act ? co_off[o + 1] - co_off[o] - 1u : 0u;
-        const bool vis = act && k == dl;
-        uint32_t v = 0;
-        if (act && !vis) {  // k-th member of D in index order
-          uint32_t kk = k;
-          bool found = false;
+        for (int w = 0; w < MW; ++w) Dr[w] = __shfl(D[w], (int)ol);
+        const uint32_t dl = __shfl(dlen, (int)ol);
+        for (uint32_t c0 = 0; c0 <= a.half_m; c0 += S) {  // jobs 0..|D| (|D| <= half_m)
+          const uint32_t k = c0 + (lane & (S - 1u));
+          const bool act = oi < npend && k <= dl;
+          const bool vis = act && k == dl;
+          uint32_t v = 0;
+          if (act && !vis) {  // k-th member of D in index order
+            uint32_t kk = k;
+            bool found = false;
 #pragma unroll
-          for (int w = 0; w < MW; ++w) {
-            uint32_t c = Dr[w];
-            const uint32_t pc = (uint32_t)__popc(c);
-            if (!found && kk < pc) {
-              for (uint32_t i = 0; i < kk; ++i) c &= c - 1u;
-              v = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(c);
-              found = true;
-            } else if (!found) {
-              kk -= pc;
+            for (int w = 0; w < MW; ++w) {
+              uint32_t c = Dr[w];
+              const uint32_t pc = (uint32_t)__popc(c);
+              if (!found && kk < pc) {
+                for (uint32_t i = 0; i < kk; ++i) c &= c - 1u;
+                v = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(c);
+                found = true;
+              } else if (!found) {
+                kk -= pc;
+              }
             }
           }
-        }
-        uint32_t Y[MW];
+          uint32_t Y[MW];
 #pragma unroll
-        for (int w = 0; w < MW; ++w) {
-          if (!act) Y[w] = 0u;
-          else if (vis) Y[w] = a.scc_mask[w] & ~Dr[w];   // visitor: scc \ Q, outside available
-          else Y[w] = Dr[w];
-        }
-        if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
-        const bool ne = EV::template gfp<2>(f, Y, vis ? 1u : 0u, rounds);
-        if (act && !vis && ne) atomicOr(&co_NE[(v >> 5) * WAVE + o], 1u << (v & 31u));
-        if (vis) {
+          for (int w = 0; w < MW; ++w) {
+            if (!act) Y[w] = 0u;
+            else if (vis) Y[w] = a.scc_mask[w] & ~Dr[w];  // visitor: scc \ Q, outside available
+            else Y[w] = Dr[w];
+          }
+          if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
+          const bool ne = EV::template gfp<2>(f, Y, vis ? 1u : 0u, rounds);
+          if (act && !vis && ne) atomicOr(&co_NE[(v >> 5) * WAVE + oi], 1u << (v & 31u));
+          if (vis) {
 #pragma unroll
-          for (int w = 0; w < MW; ++w) co_VIS[w * WAVE + o] = Y[w];
+            for (int w = 0; w < MW; ++w) co_VIS[w * WAVE + oi] = Y[w];
+          }
+          if (c0 + S > a.half_m) break;
         }
       }
       __syncthreads();
@@ -733,13 +762,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
               }
               wv[MW] = depth;
               wv[MW + 1] = dlen;
-              for (uint32_t i = 0; i < (uint32_t)WL::ORDW; ++i) {
-                uint32_t word = 0;
-#pragma unroll
-                for (uint32_t jj = 0; jj < 4; ++jj)
-                  if (i * 4 + jj < dlen) word |= (uint32_t)DO_(i * 4 + jj) << (8 * jj);
-                wv[2 * MW + 2 + i] = word;
-              }
+              for (uint32_t i = 0; i < (dlen + 3) / 4; ++i) wv[2 * MW + 2 + i] = DOW_(i);
             } else {
               atomicOr(&a.counters[3], FLAG_WIT_OVERFLOW);
             }
@@ -747,12 +770,16 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             nst = 0;  // everything left in this unit follows the witness in preorder
           }
         } else {  // not minimal: isMinimal stops at the first removable vertex in D order
-          uint32_t pos = 0;
-          for (uint32_t i = 0; i < dlen; ++i) {
-            const uint32_t v = DO_(i);
-            if ((NE[v >> 5] >> (v & 31u)) & 1u) {
-              pos = i;
-              break;
+          uint32_t pos = 0xFFFFFFFFu;
+#pragma unroll
+          for (int i = 0; i < OW; ++i) {
+            if ((uint32_t)i * 4u >= dlen) break;
+            const uint32_t word = DOW_(i);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+              const uint32_t p = (uint32_t)i * 4u + j;
+              const uint32_t v = (word >> (8 * j)) & 255u;
+              if (pos == 0xFFFFFFFFu && p < dlen && ((NE[v >> 5] >> (v & 31u)) & 1u)) pos = p;
             }
           }
           seg_evals += 2u + pos;  // cpp:184 + (pos+1) x cpp:192
@@ -760,6 +787,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
       __syncthreads();
     }
+    QI_STAMP(5);  // quorum-leaf phase
   }
 
   // units claimed by this wave's ring but never fetched: carry them over unchanged
@@ -806,9 +834,12 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     atomicAdd(&a.totals[5], (unsigned long long)tot_fetched);
     atomicAdd(&a.totals[6], (unsigned long long)wave_iters);
     atomicAdd(&a.totals[7], (unsigned long long)coop_phases);
+#ifdef QI_STAMPS
+    for (int q = 0; q < 6; ++q) atomicAdd(&a.totals[8 + q], (unsigned long long)stamp_sum[q]);
+#endif
   }
 #undef ST_
-#undef DO_
+#undef DOW_
 #undef UR_
 }
 

@@ -140,7 +140,8 @@ class DeviceSearch(SearchBackend):
             k = (ctypes.c_uint32 * self.key_words)(*key[0])
             self._c.check(self.L.qi_search_reduce(self.h, k, key[1], ctypes.byref(t)))
         return {"nodes": t.nodes, "evals": t.evals, "minq": t.minq, "zero_fallback": t.zero_fallback,
-                "rounds": t.rounds, "units": t.units, "wave_iters": t.wave_iters, "coop_phases": t.coop_phases}
+                "rounds": t.rounds, "units": t.units, "wave_iters": t.wave_iters, "coop_phases": t.coop_phases,
+                "stamps": [int(x) for x in t.stamps]}
 
     def wait_jit(self) -> bool:
         return self.L.qi_search_wait_jit(self.h) == 1
