@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -335,6 +336,11 @@ class SearchDeviceImpl : public SearchDevice {
   SearchDeviceImpl(int device, const LocalFlat& f, const SearchConfig& cfg)
       : device_(device), cfg_(cfg), m_(f.m), flat_(f) {
     DeviceGuard dg(device_);
+    // tuning overrides for experiments (profiling only; defaults are the measured best)
+    if (const char* e = std::getenv("QI_GRACE")) cfg_.grace = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
+    jit_smax_ = SMAX;
+    if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(SMAX, std::atoi(e)));
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
@@ -394,6 +400,8 @@ class SearchDeviceImpl : public SearchDevice {
     HIP_CHECK(hipStreamSynchronize(stream_));
     shm_ = (size_t)(SMAX * (MW + 1) * 64 + 2 * MW * 64 + UL::WORDS * 64 + ((UL::DMAX + 3) / 4) * 64) * 4;
     shm_ = (shm_ + 15) / 16 * 16;
+    jit_shm_ = (size_t)(jit_smax_ * (MW + 1) * 64 + 2 * MW * 64 + UL::WORDS * 64 + ((UL::DMAX + 3) / 4) * 64) * 4;
+    jit_shm_ = (jit_shm_ + 15) / 16 * 16;
     HIP_CHECK(hipFuncSetAttribute((const void*)dev::search_kernel<MW, TW, SMAX>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
     if (!cfg_.max_blocks) {  // one resident wave of blocks: no second-wave tail
@@ -499,7 +507,7 @@ class SearchDeviceImpl : public SearchDevice {
     HIP_CHECK(hipEventRecord(e0_, stream_));
     if (spec) {
       void* args[] = {&a};
-      HIP_CHECK(hipModuleLaunchKernel(jit_fn_, blocks, 1, 1, 64, 1, 1, (unsigned)shm_, stream_, args, nullptr));
+      HIP_CHECK(hipModuleLaunchKernel(jit_fn_, blocks, 1, 1, 64, 1, 1, (unsigned)jit_shm_, stream_, args, nullptr));
     } else {
       hipLaunchKernelGGL((dev::search_kernel<MW, TW, SMAX>), dim3(blocks), dim3(64), shm_, stream_, a);
     }
@@ -747,7 +755,8 @@ class SearchDeviceImpl : public SearchDevice {
   uint32_t* wit_ = nullptr;
   uint32_t wit_cap_ = 0, wit_seen_ = 0;
   std::vector<LogChunk> log_;
-  size_t shm_ = 0;
+  size_t shm_ = 0, jit_shm_ = 0;
+  int jit_smax_ = SMAX;
   bool has_best_ = false;
   std::vector<uint32_t> best_key_;
   uint32_t best_depth_ = 0;
@@ -767,7 +776,7 @@ class SearchDeviceImpl : public SearchDevice {
 
   void start_jit() {
     jit_state_.store(1);
-    std::string src = jit_source(flat_, MW, TW, SMAX, cfg_.jit == 3);
+    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3);
     jit_thread_ = std::thread([this, src]() {
       std::vector<char> code = jit_compile(src, &jit_log_);
       jit_code_ = std::move(code);
@@ -788,7 +797,7 @@ class SearchDeviceImpl : public SearchDevice {
     jit_state_.store(4);
     if (!cfg_.max_blocks) {
       int nb = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jit_fn_, 64, shm_) == hipSuccess && nb > 0)
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jit_fn_, 64, jit_shm_) == hipSuccess && nb > 0)
         max_blocks_ = cus_ * (uint32_t)nb;
     }
   }

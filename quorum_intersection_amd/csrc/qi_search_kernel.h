@@ -311,6 +311,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   constexpr int SE = MW + 1;  // stack entry words: T'[MW], packed(b, depth, dlen)
 
   constexpr int OW = (DMAX + 3) / 4;  // packed D-order words (4 vertex bytes each)
+  (void)OW;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* st = lds;                                          // [SMAX][SE][64]
   uint32_t* co_NE = st + SMAX * SE * WAVE;                      // [MW][64] per pending rank
@@ -702,23 +703,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           const uint32_t k = c0 + (lane & (S - 1u));
           const bool act = oi < npend && k <= dl;
           const bool vis = act && k == dl;
+          // job k < |D| removes the k-th vertex of the owner's D order (its LDS bytes);
+          // NE is indexed by that position, so isMinimal's first hit is one ctz
           uint32_t v = 0;
-          if (act && !vis) {  // k-th member of D in index order
-            uint32_t kk = k;
-            bool found = false;
-#pragma unroll
-            for (int w = 0; w < MW; ++w) {
-              uint32_t c = Dr[w];
-              const uint32_t pc = (uint32_t)__popc(c);
-              if (!found && kk < pc) {
-                for (uint32_t i = 0; i < kk; ++i) c &= c - 1u;
-                v = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(c);
-                found = true;
-              } else if (!found) {
-                kk -= pc;
-              }
-            }
-          }
+          if (act && !vis) v = (dow[(k >> 2) * WAVE + ol] >> (8u * (k & 3u))) & 255u;
           uint32_t Y[MW];
 #pragma unroll
           for (int w = 0; w < MW; ++w) {
@@ -728,7 +716,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           }
           if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
           const bool ne = EV::template gfp<2>(f, Y, vis ? 1u : 0u, rounds);
-          if (act && !vis && ne) atomicOr(&co_NE[(v >> 5) * WAVE + oi], 1u << (v & 31u));
+          if (act && !vis && ne) atomicOr(&co_NE[(k >> 5) * WAVE + oi], 1u << (k & 31u));
           if (vis) {
 #pragma unroll
             for (int w = 0; w < MW; ++w) co_VIS[w * WAVE + oi] = Y[w];
@@ -770,18 +758,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             nst = 0;  // everything left in this unit follows the witness in preorder
           }
         } else {  // not minimal: isMinimal stops at the first removable vertex in D order
-          uint32_t pos = 0xFFFFFFFFu;
+          uint32_t pos = 0;
 #pragma unroll
-          for (int i = 0; i < OW; ++i) {
-            if ((uint32_t)i * 4u >= dlen) break;
-            const uint32_t word = DOW_(i);
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-              const uint32_t p = (uint32_t)i * 4u + j;
-              const uint32_t v = (word >> (8 * j)) & 255u;
-              if (pos == 0xFFFFFFFFu && p < dlen && ((NE[v >> 5] >> (v & 31u)) & 1u)) pos = p;
-            }
-          }
+          for (int w = MW - 1; w >= 0; --w)
+            if (NE[w]) pos = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(NE[w]);
           seg_evals += 2u + pos;  // cpp:184 + (pos+1) x cpp:192
         }
       }
