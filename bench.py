@@ -80,6 +80,12 @@ def main():
     ap.add_argument("--grow-budget", type=int, default=0)
     ap.add_argument("--run-budget", type=int, default=0)
     ap.add_argument("--max-blocks", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=0,
+                    help="launches per chain between host synchronisations (0: 64 at N=1, 8 at N>1)")
+    ap.add_argument("--seed-units", type=int, default=0,
+                    help="N>1: units rank 0 grows and deals out (0 = 2048 per rank)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI) for the measurement; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--jit", type=int, default=2,
                     help="0 auto, 1 table-interpreting kernel only, 2 run-time specialised kernel (default)")
     args = ap.parse_args()
@@ -96,28 +102,36 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one GPU per rank; the modulo only matters when rehearsing N>1 (gloo) on a 1-GPU box
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    comm_dev = dev
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
+            comm_dev = torch.device("cpu")
+    batch = args.batch or (64 if world == 1 else 8)
 
     text = fbas_gen.two_tier(args.k_top, args.validators)
 
     # ---- time-to-verdict from JSON text (host parse + flatten + upload + solve), N=1 path
     t0 = time.perf_counter()
-    fb = qa.FBAS(text, device=local)
+    fb = qa.FBAS(text, device=gpu)
     ttv_res = fb.solve_stats(args.grow_budget, args.run_budget, args.max_blocks)  # jit auto (CLI default)
     time_to_verdict = time.perf_counter() - t0
 
-    be = DeviceSearch(fb, args.grow_budget, args.run_budget, args.max_blocks, jit=args.jit)
+    be = DeviceSearch(fb, args.grow_budget, args.run_budget, args.max_blocks, jit=args.jit, batch=batch)
     shape = be.shape()
     sccs = fb.sccs()
     scc_masks = qa.masks_from_sets(sccs, fb.n)
 
     def one_step():
         fb.gfp_batch(scc_masks, scc_masks)          # per-SCC checks (cpp:649-672)
-        return distributed_search(be, device=dev)   # search (cpp:691 -> 348-400)
+        return distributed_search(be, device=comm_dev, seed_units=args.seed_units)  # search (cpp:691 -> 348-400)
 
     for _ in range(args.warmup):
         one_step()
@@ -138,7 +152,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms, float(launches)], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kernel_ms, float(launches)], dtype=torch.float64, device=comm_dev)
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
@@ -192,7 +206,8 @@ def main():
             "search_nodes_per_step": res.nodes,
             "evals_per_step": evals_per_step,
             "verdict": res.verdict,
-            "parallelism": f"search-tree sharding x{world} (RCCL all_gather + send/recv)",
+            "parallelism": (f"search-tree sharding x{world}: rank-0 frontier broadcast, strided shares, "
+                            f"{args.dist_backend} all_gather + send/recv between chains of {batch} launches"),
         },
         "roofline": {
             "bound": "valu",

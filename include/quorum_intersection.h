@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define QI_ABI_VERSION 1
+#define QI_ABI_VERSION 2
 
 enum {
   QI_OK = 0,
@@ -86,6 +86,8 @@ typedef struct {
   uint32_t jit;            /* run-time specialised search kernel: 0 auto (background compile
                               once a search needs >= 3 launches), 1 off, 2 before launch 1,
                               3 = 2 + diagnostic section stamps (not for measurement) */
+  uint32_t batch;          /* 0 = default: search launches chained on the device per host
+                              synchronisation (each reads its input count from the previous) */
 } qi_solve_opts;
 
 typedef struct {
@@ -136,6 +138,7 @@ void qi_free(void* p);
 typedef struct {
   uint32_t grow_budget, run_budget, max_blocks; /* 0 = defaults */
   uint32_t jit;                                  /* as qi_solve_opts.jit */
+  uint32_t batch;                                /* launches per qi_search_step (0 = default) */
 } qi_search_opts;
 
 typedef struct {
@@ -143,8 +146,8 @@ typedef struct {
   uint32_t budget, blocks;
   uint64_t new_witnesses;
   double kernel_ms;
-  uint32_t specialized;  /* 1 if this launch ran the run-time specialised kernel */
-  uint32_t pad;
+  uint32_t specialized;  /* 1 if this step ran the run-time specialised kernel */
+  uint32_t launches;     /* chained launches of this step that had input */
 } qi_step_info;
 
 typedef struct {
@@ -178,9 +181,15 @@ uint32_t qi_search_unit_bytes(const qi_search* s);
 uint32_t qi_search_key_words(const qi_search* s);  /* 32-bit words of a path key */
 int qi_search_reset(qi_search* s);                  /* frontier = {root} (cpp:393) */
 int qi_search_clear(qi_search* s);                  /* frontier = {} */
+/* One batch of chained launches (qi_search_opts.batch), one host synchronisation. */
 int qi_search_step(qi_search* s, qi_step_info* info);
+/* As qi_search_step, but stops enqueueing once a finished launch left >= target units
+ * (rank 0 grows the frontier it hands out to the other ranks). */
+int qi_search_grow(qi_search* s, uint64_t target, qi_step_info* info);
 uint64_t qi_search_frontier(const qi_search* s);
 int qi_search_keep_slice(qi_search* s, uint64_t begin, uint64_t end);
+/* Keep units offset, offset + stride, ... (a rank's share of a broadcast frontier). */
+int qi_search_keep_strided(qi_search* s, uint64_t offset, uint64_t stride);
 int qi_search_export(qi_search* s, uint64_t count, void* device_dst); /* pop `count` from the tail */
 int qi_search_import(qi_search* s, uint64_t count, const void* device_src);
 /* Best witness found locally: key[key_words], depth; returns 1 if any. */

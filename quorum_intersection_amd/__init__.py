@@ -58,6 +58,7 @@ class FBAS:
         h = ctypes.c_void_p()
         check(lib().qi_fbas_from_json(data, len(data), device, ctypes.byref(h)))
         self._h = h
+        self.device = device
         self.n = int(lib().qi_fbas_num_vertices(h))
 
     def close(self):
@@ -123,10 +124,11 @@ class FBAS:
         return [v for v in nodes if v in keep]
 
     # ---- device: solve / search -------------------------------------------------------
-    def solve_stats(self, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0, jit: int = 0) -> Dict:
+    def solve_stats(self, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0, jit: int = 0,
+                    batch: int = 0) -> Dict:
         """jit: 0 auto (specialised kernel compiled in the background for long searches),
         1 table-interpreting kernel only, 2 specialised kernel from the first launch."""
-        opts = _capi.SolveOpts(0, grow_budget, run_budget, max_blocks, jit)
+        opts = _capi.SolveOpts(0, grow_budget, run_budget, max_blocks, jit, batch)
         res = _capi.SolveResult()
         q1 = np.zeros(max(self.n, 1), dtype=np.uint32)
         q2 = np.zeros(max(self.n, 1), dtype=np.uint32)

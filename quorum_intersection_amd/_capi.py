@@ -29,7 +29,7 @@ class QIError(RuntimeError):
 
 class SolveOpts(ctypes.Structure):
     _fields_ = [("tiebreak", c_uint32), ("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32),
-                ("jit", c_uint32)]
+                ("jit", c_uint32), ("batch", c_uint32)]
 
 
 class SolveResult(ctypes.Structure):
@@ -58,7 +58,8 @@ class SolveResult(ctypes.Structure):
 
 
 class SearchOpts(ctypes.Structure):
-    _fields_ = [("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32), ("jit", c_uint32)]
+    _fields_ = [("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32), ("jit", c_uint32),
+                ("batch", c_uint32)]
 
 
 class StepInfo(ctypes.Structure):
@@ -71,7 +72,7 @@ class StepInfo(ctypes.Structure):
         ("new_witnesses", c_uint64),
         ("kernel_ms", c_double),
         ("specialized", c_uint32),
-        ("pad", c_uint32),
+        ("launches", c_uint32),
     ]
 
 
@@ -114,6 +115,8 @@ SIGNATURES = {
     "qi_search_step": (c_int, [c_void_p, POINTER(StepInfo)]),
     "qi_search_frontier": (c_uint64, [c_void_p]),
     "qi_search_keep_slice": (c_int, [c_void_p, c_uint64, c_uint64]),
+    "qi_search_grow": (c_int, [c_void_p, c_uint64, POINTER(StepInfo)]),
+    "qi_search_keep_strided": (c_int, [c_void_p, c_uint64, c_uint64]),
     "qi_search_export": (c_int, [c_void_p, c_uint64, c_void_p]),
     "qi_search_import": (c_int, [c_void_p, c_uint64, c_void_p]),
     "qi_search_local_best": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
@@ -142,7 +145,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.qi_abi_version() != 1:
+        if L.qi_abi_version() != 2:
             raise ImportError("libqi_amd.so ABI version mismatch")
         _lib = L
     return _lib

@@ -96,9 +96,10 @@ std::vector<uint32_t> scc_quorum_check(qi_fbas* f, std::vector<std::vector<uint3
   return with;
 }
 
-qi::SearchConfig make_cfg(uint32_t grow, uint32_t run, uint32_t blocks, uint32_t jit = 0) {
+qi::SearchConfig make_cfg(uint32_t grow, uint32_t run, uint32_t blocks, uint32_t jit = 0, uint32_t batch = 0) {
   qi::SearchConfig c;
   c.jit = jit;
+  if (batch) c.batch = batch;
   if (grow) c.grow_budget = grow;
   if (run) c.run_budget = run;
   if (blocks) c.max_blocks = blocks;
@@ -121,7 +122,7 @@ SearchOutcome run_search(qi_fbas* f, const qi::SearchConfig& cfg) {
   const auto& scc = f->sccs.members.front();
   qi::LocalFlat lf = qi::flatten_local(f->g, scc);
   auto sd = qi::make_search_device(f->device, lf, cfg);
-  while (sd->frontier_size()) sd->step();
+  while (sd->frontier_size()) sd->step(0);
   SearchOutcome o;
   o.nonmonotone = lf.nonmonotone;
   qi::Witness w;
@@ -215,7 +216,7 @@ int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32
     }
     res->searched = 1;
     qi::SearchConfig cfg = make_cfg(opts ? opts->grow_budget : 0, opts ? opts->run_budget : 0,
-                                    opts ? opts->max_blocks : 0, opts ? opts->jit : 0);
+                                    opts ? opts->max_blocks : 0, opts ? opts->jit : 0, opts ? opts->batch : 0);
     auto t1 = std::chrono::steady_clock::now();
     SearchOutcome o = run_search(f, cfg);
     res->t_search_ms = ms_since(t1);
@@ -324,7 +325,8 @@ int qi_search_create(qi_fbas* f, const qi_search_opts* opts, qi_search** out) {
     s->lf = qi::flatten_local(f->g, f->sccs.members.front());
     s->sd = qi::make_search_device(f->device, s->lf,
                                    make_cfg(opts ? opts->grow_budget : 0, opts ? opts->run_budget : 0,
-                                            opts ? opts->max_blocks : 0, opts ? opts->jit : 0));
+                                            opts ? opts->max_blocks : 0, opts ? opts->jit : 0,
+                                            opts ? opts->batch : 0));
     *out = s.release();
     return QI_OK;
   });
@@ -344,10 +346,10 @@ int qi_search_clear(qi_search* s) {
   return guarded([&] { s->sd->clear_frontier(); return QI_OK; });
 }
 
-int qi_search_step(qi_search* s, qi_step_info* info) {
+static int search_step(qi_search* s, uint64_t until, qi_step_info* info) {
   if (!s) return fail(QI_ERR_ARG, "null");
   return guarded([&] {
-    qi::StepInfo si = s->sd->step();
+    qi::StepInfo si = s->sd->step(until);
     if (info) {
       info->frontier_in = si.frontier_in;
       info->frontier_out = si.frontier_out;
@@ -357,13 +359,23 @@ int qi_search_step(qi_search* s, qi_step_info* info) {
       info->new_witnesses = si.new_witnesses;
       info->kernel_ms = si.kernel_ms;
       info->specialized = si.specialized ? 1u : 0u;
-      info->pad = 0;
+      info->launches = si.launches;
     }
     return QI_OK;
   });
 }
 
+int qi_search_step(qi_search* s, qi_step_info* info) { return search_step(s, 0, info); }
+int qi_search_grow(qi_search* s, uint64_t target, qi_step_info* info) {
+  return search_step(s, target ? target : 1, info);
+}
+
 uint64_t qi_search_frontier(const qi_search* s) { return s ? s->sd->frontier_size() : 0; }
+
+int qi_search_keep_strided(qi_search* s, uint64_t offset, uint64_t stride) {
+  if (!s || stride == 0) return fail(QI_ERR_ARG, "null or stride 0");
+  return guarded([&] { s->sd->keep_strided(offset, stride); return QI_OK; });
+}
 
 int qi_search_keep_slice(qi_search* s, uint64_t begin, uint64_t end) {
   if (!s) return fail(QI_ERR_ARG, "null");

@@ -26,14 +26,17 @@ std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g);
 // Branch-and-bound search (iterateMinimalQuorums + checkMinimalQuorums, cpp:252-400)
 // as a budgeted frontier loop.  A "unit" is a subtree root (T, D, path key, D order);
 // one launch runs a per-lane depth-first walk of units for at most `budget` search
-// nodes per lane, spilling the rest of its stack back into the next frontier.
+// nodes per lane, spilling the rest of its stack back into the next frontier.  Launches
+// are chained on the device; step() enqueues a batch of them and synchronises once.
 // ----------------------------------------------------------------------------------
 struct SearchConfig {
   uint32_t max_blocks = 0;       // 0 = CUs * 8
-  uint32_t grow_budget = 48;     // per-lane node budget while the frontier is small
+  uint32_t grow_budget = 4;      // per-lane node budget while the frontier is small (sweep: 4 < 8 < 16 < 48 ms)
   uint32_t run_budget = 4096;    // per-lane node budget once the frontier fills the GPU
   uint32_t grace = 64;           // per-lane steps after the unit queue runs dry
   uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output)
+  uint32_t batch = 0;            // max chained launches per step() (0 = 64)
+  uint32_t lookahead = 2;        // launches kept in flight beyond the one the host waits for
   bool keep_log = true;          // keep per-segment records for preorder-exact counts
   // Run-time specialised kernel (qi_jit.cpp): 0 = auto (compile in the background once a
   // search reaches `jit_after` launches, switch at the next launch boundary), 1 = off
@@ -45,7 +48,8 @@ struct SearchConfig {
 
 struct StepInfo {
   uint64_t frontier_in = 0, frontier_out = 0;
-  uint64_t processed = 0;        // units fetched this launch
+  uint64_t processed = 0;        // input units of the launches of this step
+  uint32_t launches = 0;         // launches that had input (the rest of the batch was empty)
   uint32_t budget = 0, blocks = 0;
   uint64_t new_witnesses = 0;
   double kernel_ms = 0;          // HIP-event time of the search kernel
@@ -73,13 +77,16 @@ class SearchDevice {
   virtual uint32_t unit_bytes() const = 0;
   virtual void reset_root() = 0;                    // frontier = {root of cpp:393}
   virtual void clear_frontier() = 0;
-  virtual StepInfo step() = 0;                      // one launch + compaction
+  // One chain of launches; with until > 0 the host stops enqueueing once a finished
+  // launch left at least `until` units (frontier growth for multi-rank hand-out).
+  virtual StepInfo step(uint64_t until = 0) = 0;
   virtual uint64_t frontier_size() const = 0;
   // Frontier hand-off for multi-rank rebalancing: units are moved through caller-owned
   // device memory (e.g. torch tensors sent with RCCL).
   virtual void export_tail(uint64_t count, void* dev_dst) = 0;
   virtual void import_units(uint64_t count, const void* dev_src) = 0;
   virtual void keep_slice(uint64_t begin, uint64_t end) = 0;
+  virtual void keep_strided(uint64_t offset, uint64_t stride) = 0;  // units offset, offset+stride, ...
   // Global best (preorder-first witness key) known to the caller, for pruning.
   virtual void set_best(const std::vector<uint32_t>& key, uint32_t depth) = 0;
   virtual bool best(Witness* w) const = 0;          // best witness found on this device

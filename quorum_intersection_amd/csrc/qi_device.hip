@@ -56,20 +56,25 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
   search_body<MW, TW, SMAX, TableEval<MW, TW>>(a);
 }
 
-// Zero-record the units never claimed from the global head (host carries them over).
+// out[i] = in[offset + i * stride]: a rank's strided share of a broadcast frontier.
 template <int MW>
-__global__ void zero_records_kernel(uint32_t* records, uint32_t from, uint32_t to) {
-  const uint32_t i = from + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < to) {
-    uint32_t* r = records + (size_t)i * RecLayout<MW>::WORDS;
-    for (int w = 0; w < RecLayout<MW>::WORDS; ++w) r[w] = 0u;
+__global__ void gather_units_kernel(const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt, uint32_t* out) {
+  using UL = UnitLayout<MW>;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4* s4 = (const uint4*)(in + (offset + i * stride) * UL::WORDS);
+    uint4* d4 = (uint4*)(out + i * UL::WORDS);
+#pragma unroll
+    for (int q = 0; q < UL::WORDS / 4; ++q) d4[q] = s4[q];
   }
 }
 
 // Preorder-filtered sums over a log chunk: segment roots at or before (key, depth).
+// Wave shuffles, then one LDS combine per block and one atomic per value per block (a
+// same-address atomic per wave serialised ~65K atomics at the L2: 0.53 ms per reduce).
 template <int MW>
-__global__ void reduce_kernel(const uint32_t* records, uint64_t n, uint32_t has_key, const uint32_t* key,
-                              uint32_t depth, unsigned long long* out) {
+__global__ __launch_bounds__(256) void reduce_kernel(const uint32_t* records, uint64_t n, uint32_t has_key,
+                                                     const uint32_t* key, uint32_t depth, unsigned long long* out) {
+  __shared__ unsigned long long part[4][4];
   uint64_t s[4] = {0, 0, 0, 0};
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t* r = records + i * RecLayout<MW>::WORDS;
@@ -82,11 +87,18 @@ __global__ void reduce_kernel(const uint32_t* records, uint64_t n, uint32_t has_
     s[2] += r[MW + 3];
     s[3] += r[MW + 4];
   }
+  const uint32_t wv = threadIdx.x >> 6;
   for (int q = 0; q < 4; ++q) {
     uint64_t v = s[q];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&out[q], (unsigned long long)v);
+    if ((threadIdx.x & 63) == 0) part[wv][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    unsigned long long v = 0;
+    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) v += part[w][threadIdx.x];
+    if (v) atomicAdd(&out[threadIdx.x], v);
   }
 }
 
@@ -387,14 +399,21 @@ class SearchDeviceImpl : public SearchDevice {
 
     cus_ = (uint32_t)device_cu_count(device_);
     max_blocks_ = cfg_.max_blocks ? cfg_.max_blocks : cus_ * 8u;  // refined below once shm_ is known
-    counters_ = dalloc<uint32_t>(4);
-    totals_ = dalloc<unsigned long long>(16);
+    ctr_ = dalloc<uint32_t>((size_t)(kMaxBatch + 1) * dev::CTR_WORDS);
+    glob_ = dalloc<uint32_t>(2);
+    HIP_CHECK(hipMemsetAsync(glob_, 0, 8, stream_));
+    HIP_CHECK(hipHostMalloc((void**)&hctr_, (size_t)kMaxBatch * dev::HC_WORDS * 4 + 64,
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_CHECK(hipHostGetDevicePointer((void**)&hctr_dev_, (void*)hctr_, 0));
+    glob_host_ = hctr_ + (size_t)kMaxBatch * dev::HC_WORDS;
+    for (auto& e : ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDefault));
+    totals_ = dalloc<unsigned long long>(16 * dev::TOT_SHARDS);
     best64_ = dalloc<unsigned long long>(1);
     red_ = dalloc<unsigned long long>(4);
     keydev_ = dalloc<uint32_t>(8);
     wit_cap_ = 1u << 16;
     wit_ = dalloc<uint32_t>((size_t)wit_cap_ * WL::WORDS);
-    HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * sizeof(unsigned long long), stream_));
+    HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * dev::TOT_SHARDS * sizeof(unsigned long long), stream_));
     unsigned long long inf = ~0ull;
     HIP_CHECK(hipMemcpyAsync(best64_, &inf, 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -424,7 +443,10 @@ class SearchDeviceImpl : public SearchDevice {
     for (auto* p : bufs_) (void)hipFree(p);
     for (int i = 0; i < 2; ++i) (void)hipFree(units_[i]);
     for (auto& c : log_) (void)hipFree(c.ptr);
-    (void)hipFree(counters_);
+    (void)hipFree(ctr_);
+    (void)hipFree(glob_);
+    (void)hipHostFree((void*)hctr_);
+    for (auto& e : ev_) (void)hipEventDestroy(e);
     (void)hipFree(totals_);
     (void)hipFree(best64_);
     (void)hipFree(red_);
@@ -452,35 +474,60 @@ class SearchDeviceImpl : public SearchDevice {
 
   uint64_t frontier_size() const override { return n_; }
 
-  StepInfo step() override {
+  // One step = a chain of up to `batch` launches (see C_* in qi_search_kernel.h).  Every
+  // launch reads its input count and log position from the previous launch's counter
+  // block on the device, so the host only enqueues.  It keeps `lookahead` launches in
+  // flight beyond the one it waits for; the last block of each launch publishes that
+  // launch's counters into pinned host memory, so the host sees the frontier run empty
+  // (or a capacity stop) without a copy and stops enqueueing: at most `lookahead` empty
+  // launches trail a search.  A launch that could exceed the unit or log capacity does
+  // nothing, and neither does the rest of the chain; the host grows the buffers and
+  // resumes from that launch's input.
+  StepInfo step(uint64_t until) override {
     DeviceGuard dg(device_);
     StepInfo si;
     si.frontier_in = n_;
     if (n_ == 0) return si;
-    const uint32_t lanes_full = max_blocks_ * 64u;
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n_ + 63) / 64, max_blocks_);
-    const uint32_t budget = (n_ >= (uint64_t)lanes_full / 2) ? cfg_.run_budget : cfg_.grow_budget;
-    const uint64_t lanes = (uint64_t)blocks * 64u;
-    const uint64_t out_need = n_ + lanes * (SMAX + 1 + cfg_.evict_max);
-    if (out_need > 0xFFFFFFF0ull) throw Error(QI_ERR_CAPACITY, "search frontier exceeds 2^32 units");
-    ensure_cap(1 - cur_, out_need);
-    uint32_t* rec = log_reserve(n_);
-    uint32_t init[4] = {0, (uint32_t)std::min<uint64_t>(n_, lanes), 0, 0};
-    HIP_CHECK(hipMemcpyAsync(counters_, init, sizeof init, hipMemcpyHostToDevice, stream_));
+    // run-time specialised kernel: start compiling once the search proves non-trivial,
+    // switch to it at the first step boundary after it is ready
+    if (cfg_.jit == 0 && launches_ >= cfg_.jit_after && jit_state_.load() == 0 && jit_eligible(flat_)) start_jit();
+    if (jit_state_.load() == 2) load_jit();
+    const bool spec = jit_fn_ != nullptr;
+    const uint32_t smax = spec ? (uint32_t)jit_smax_ : (uint32_t)SMAX;
+    const uint32_t blocks = max_blocks_;
+    const uint32_t K = std::max(1u, std::min(cfg_.batch ? cfg_.batch : (uint32_t)kMaxBatch, (uint32_t)kMaxBatch));
+    const uint32_t D = std::max(1u, cfg_.lookahead);
+    auto first_need = [&](uint64_t n) {
+      const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
+      return n + nb * 64u * (smax + 1 + cfg_.evict_max);
+    };
+    {
+      const uint64_t need = first_need(n_);
+      if (need > 0xFFFFFFF0ull) throw Error(QI_ERR_CAPACITY, "search frontier exceeds 2^32 units");
+      ensure_cap(cur_, need, true);
+      ensure_cap(1 - cur_, need);
+      if (log_.empty() || log_.back().cap - log_.back().used < n_) new_log_chunk(n_);
+    }
+    LogChunk& lc = log_.back();
+    uint32_t seed[dev::CTR_WORDS] = {0};
+    seed[dev::C_OUT] = (uint32_t)n_;
+    seed[dev::C_LOGB] = (uint32_t)lc.used;
+    HIP_CHECK(hipMemcpyAsync(ctr_, seed, sizeof seed, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemsetAsync(ctr_ + dev::CTR_WORDS, 0, (size_t)K * dev::CTR_WORDS * 4, stream_));
+    std::memset((void*)hctr_, 0, (size_t)K * dev::HC_WORDS * 4);
 
     dev::SearchArgs a{};
     a.f = d_;
-    a.units_in = units_[cur_];
-    a.n_in = (uint32_t)n_;
-    a.units_out = units_[1 - cur_];
-    a.out_cap = (uint32_t)cap_[1 - cur_];
-    a.counters = counters_;
-    a.records = rec;
+    a.out_cap = (uint32_t)std::min<uint64_t>(cap_[0], cap_[1]);
+    a.log_cap = (uint32_t)std::min<uint64_t>(lc.cap, 0xFFFFFFF0ull);
+    a.glob = glob_;
+    a.records = lc.ptr;
     a.wit = wit_;
     a.wit_cap = wit_cap_;
     a.totals = totals_;
     a.best64 = best64_;
-    a.budget = budget;
+    a.grow_budget = cfg_.grow_budget;
+    a.run_budget = cfg_.run_budget;
     a.grace = cfg_.grace;
     a.evict_max = cfg_.evict_max;
     a.half_m = m_ / 2;
@@ -499,66 +546,94 @@ class SearchDeviceImpl : public SearchDevice {
       a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
       a.scc_mask[w] = scc_mask_[w];
     }
-    // run-time specialised kernel: start compiling once the search proves non-trivial,
-    // switch to it at the first launch boundary after it is ready
-    if (cfg_.jit == 0 && launches_ >= cfg_.jit_after && jit_state_.load() == 0 && jit_eligible(flat_)) start_jit();
-    if (jit_state_.load() == 2) load_jit();
-    const bool spec = jit_fn_ != nullptr;
-    HIP_CHECK(hipEventRecord(e0_, stream_));
-    if (spec) {
-      void* args[] = {&a};
-      HIP_CHECK(hipModuleLaunchKernel(jit_fn_, blocks, 1, 1, 64, 1, 1, (unsigned)jit_shm_, stream_, args, nullptr));
-    } else {
-      hipLaunchKernelGGL((dev::search_kernel<MW, TW, SMAX>), dim3(blocks), dim3(64), shm_, stream_, a);
-    }
-    HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipEventRecord(e1_, stream_));
-    si.specialized = spec;
-    if (spec) ++spec_launches_;
-    uint32_t c[4];
-    HIP_CHECK(hipMemcpyAsync(c, counters_, sizeof c, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
-    float ms = 0;
-    HIP_CHECK(hipEventElapsedTime(&ms, e0_, e1_));
-    if (c[3] & dev::FLAG_OUT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "search frontier buffer overflow");
-    if (c[3] & dev::FLAG_WIT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "witness buffer overflow");
-    uint64_t out = c[0];
-    const uint64_t head = std::min<uint64_t>(c[1], n_);
-    if (head < n_) {  // never-claimed units: zero their records and carry them over
-      const uint64_t left = n_ - head;
-      if (out + left > cap_[1 - cur_]) throw Error(QI_ERR_CAPACITY, "search frontier buffer overflow");
-      HIP_CHECK(hipMemcpyAsync(units_[1 - cur_] + out * UL::WORDS, units_[cur_] + head * UL::WORDS,
-                               left * UL::BYTES, hipMemcpyDeviceToDevice, stream_));
-      const uint32_t nb = (uint32_t)((left + 255) / 256);
-      hipLaunchKernelGGL(dev::zero_records_kernel<MW>, dim3(nb), dim3(256), 0, stream_, rec, (uint32_t)head,
-                         (uint32_t)n_);
+    HIP_CHECK(hipEventRecord(ev_[0], stream_));
+    auto enqueue = [&](uint32_t k) {
+      a.units_in = units_[(cur_ + k) & 1];
+      a.units_out = units_[(cur_ + k + 1) & 1];
+      a.prev = ctr_ + (size_t)k * dev::CTR_WORDS;
+      a.counters = ctr_ + (size_t)(k + 1) * dev::CTR_WORDS;
+      a.host_ctr = hctr_dev_ + (size_t)k * dev::HC_WORDS;
+      if (spec) {
+        void* args[] = {&a};
+        HIP_CHECK(hipModuleLaunchKernel(jit_fn_, blocks, 1, 1, 64, 1, 1, (unsigned)jit_shm_, stream_, args, nullptr));
+      } else {
+        hipLaunchKernelGGL((dev::search_kernel<MW, TW, SMAX>), dim3(blocks), dim3(64), shm_, stream_, a);
+      }
       HIP_CHECK(hipGetLastError());
-      out += left;
+      HIP_CHECK(hipEventRecord(ev_[k + 1], stream_));
+    };
+    auto hc = [&](uint32_t k) -> const volatile uint32_t* { return hctr_ + (size_t)k * dev::HC_WORDS; };
+    uint32_t enq = 0;
+    while (enq < K) {
+      enqueue(enq++);
+      if (enq > D) {  // wait for launch enq-1-D; stop enqueueing once the chain has run out
+        const uint32_t j = enq - 1 - D;
+        HIP_CHECK(hipEventSynchronize(ev_[j + 1]));
+        if (hc(j)[dev::HC_STOP] || hc(j)[dev::HC_OUT] == 0) break;
+        if (until && hc(j)[dev::HC_OUT] >= until) break;
+      }
     }
-    // collect new witnesses
-    if (c[2] > wit_seen_) {
-      const uint32_t nw = std::min(c[2], wit_cap_) - wit_seen_;
+    HIP_CHECK(hipMemcpyAsync((void*)glob_host_, glob_, 8, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    const uint32_t g_wit = glob_host_[0], g_flags = glob_host_[1];
+    if (g_flags & dev::FLAG_OUT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "search frontier buffer overflow");
+    if (g_flags & dev::FLAG_WIT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "witness buffer overflow");
+    // walk the chain: launches that ran, the first stopped one, the final frontier
+    uint32_t ran = 0, k = 0;
+    bool stopped = false;
+    double ms_sum = 0;
+    uint64_t n_next = n_, log_next = lc.used;
+    int cur_next = cur_;
+    for (; k < enq; ++k) {
+      const volatile uint32_t* c = hc(k);
+      if (!c[dev::HC_DONE]) throw Error(QI_ERR_DEVICE, "search launch did not publish its counters");
+      if (c[dev::HC_STOP]) {  // frontier = launch k's input
+        stopped = true;
+        break;
+      }
+      cur_next = (cur_ + k + 1) & 1;
+      n_next = c[dev::HC_OUT];
+      log_next = (uint64_t)c[dev::HC_LOGB] + c[dev::HC_NIN];
+      if (c[dev::HC_NIN] == 0) continue;
+      ++ran;
+      si.processed += c[dev::HC_NIN];
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, ev_[k], ev_[k + 1]));
+      ms_sum += ms;
+    }
+    n_ = n_next;
+    cur_ = cur_next;
+    lc.used = log_next;
+    if (stopped) {
+      const uint64_t need = first_need(n_);
+      if (need > 0xFFFFFFF0ull) throw Error(QI_ERR_CAPACITY, "search frontier exceeds 2^32 units");
+      if (need > std::min(cap_[0], cap_[1])) {
+        ensure_cap(cur_, 2 * need, true);
+        ensure_cap(1 - cur_, 2 * need);
+      }
+      if (lc.cap - lc.used < n_) new_log_chunk(2 * n_);
+      ++stops_;
+    }
+    // collect new witnesses (the buffer restarts at 0 for the next step)
+    if (g_wit > 0) {
+      const uint32_t nw = std::min(g_wit, wit_cap_);
       std::vector<uint32_t> wv((size_t)nw * WL::WORDS);
-      HIP_CHECK(hipMemcpyAsync(wv.data(), wit_ + (size_t)wit_seen_ * WL::WORDS, wv.size() * 4,
-                               hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipMemcpyAsync(wv.data(), wit_, wv.size() * 4, hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipMemsetAsync(glob_, 0, 8, stream_));
       HIP_CHECK(hipStreamSynchronize(stream_));
       for (uint32_t i = 0; i < nw; ++i) absorb_witness(&wv[(size_t)i * WL::WORDS]);
       si.new_witnesses = nw;
-      // next launch reuses the buffer from the start
-      wit_seen_ = 0;
-      HIP_CHECK(hipMemsetAsync(counters_ + 2, 0, 4, stream_));
     }
-    HIP_CHECK(hipStreamSynchronize(stream_));
-    si.processed = head;
-    si.frontier_out = out;
-    si.budget = budget;
+    si.frontier_out = n_;
+    si.budget = cfg_.run_budget;
     si.blocks = blocks;
-    si.kernel_ms = ms;
+    si.kernel_ms = ms_sum;
+    si.launches = ran;
     si.has_best = has_local_best_ || has_best_;
-    sum_ms_ += ms;
-    ++launches_;
-    n_ = out;
-    cur_ = 1 - cur_;
+    si.specialized = spec;
+    sum_ms_ += ms_sum;
+    launches_ += ran;
+    if (spec) spec_launches_ += ran;
     return si;
   }
 
@@ -591,6 +666,22 @@ class SearchDeviceImpl : public SearchDevice {
     n_ = end - begin;
   }
 
+  void keep_strided(uint64_t offset, uint64_t stride) override {
+    DeviceGuard dg(device_);
+    if (stride == 0) throw Error(QI_ERR_ARG, "keep_strided: stride 0");
+    const uint64_t cnt = offset < n_ ? (n_ - offset + stride - 1) / stride : 0;
+    if (cnt) {
+      ensure_cap(1 - cur_, cnt);
+      const uint32_t nb = (uint32_t)std::min<uint64_t>((cnt + 255) / 256, 4096);
+      hipLaunchKernelGGL(dev::gather_units_kernel<MW>, dim3(nb), dim3(256), 0, stream_, units_[cur_], offset, stride,
+                         cnt, units_[1 - cur_]);
+      HIP_CHECK(hipGetLastError());
+      cur_ = 1 - cur_;
+    }
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    n_ = cnt;
+  }
+
   void set_best(const std::vector<uint32_t>& key, uint32_t depth) override {
     best_key_ = key;
     best_key_.resize(MW, 0);
@@ -605,6 +696,8 @@ class SearchDeviceImpl : public SearchDevice {
   }
 
   Totals reduce(bool has_key, const std::vector<uint32_t>& key, uint32_t depth) override {
+    // no witness: every segment counts, and the running totals are exactly those sums
+    if (!has_key) return running_totals();
     DeviceGuard dg(device_);
     std::vector<uint32_t> k(8, 0);
     for (size_t i = 0; i < key.size() && i < 8; ++i) k[i] = key[i];
@@ -612,7 +705,7 @@ class SearchDeviceImpl : public SearchDevice {
     HIP_CHECK(hipMemsetAsync(red_, 0, 32, stream_));
     for (auto& c : log_) {
       if (!c.used) continue;
-      const uint32_t nb = (uint32_t)std::min<uint64_t>((c.used + 255) / 256, 4096);
+      const uint32_t nb = (uint32_t)std::min<uint64_t>((c.used + 255) / 256, (uint64_t)cus_ * 4u);
       hipLaunchKernelGGL(dev::reduce_kernel<MW>, dim3(nb), dim3(256), 0, stream_, c.ptr, c.used, has_key ? 1u : 0u,
                          keydev_, depth, red_);
       HIP_CHECK(hipGetLastError());
@@ -636,9 +729,12 @@ class SearchDeviceImpl : public SearchDevice {
 
   Totals running_totals() const override {
     DeviceGuard dg(device_);
-    unsigned long long r[16];
-    HIP_CHECK(hipMemcpyAsync(r, totals_, sizeof r, hipMemcpyDeviceToHost, stream_));
+    std::vector<unsigned long long> sh(16 * dev::TOT_SHARDS);
+    HIP_CHECK(hipMemcpyAsync(sh.data(), totals_, sh.size() * 8, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    unsigned long long r[16] = {0};
+    for (int q = 0; q < dev::TOT_SHARDS; ++q)
+      for (int i = 0; i < 16; ++i) r[i] += sh[(size_t)q * 16 + i];
     Totals t;
     t.nodes = r[0];
     t.evals = r[1];
@@ -655,7 +751,7 @@ class SearchDeviceImpl : public SearchDevice {
   void drop_log() override {
     for (auto& c : log_) c.used = 0;
     DeviceGuard dg(device_);
-    HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * sizeof(unsigned long long), stream_));
+    HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * dev::TOT_SHARDS * sizeof(unsigned long long), stream_));
     unsigned long long inf = ~0ull;
     HIP_CHECK(hipMemcpyAsync(best64_, &inf, 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
@@ -697,19 +793,13 @@ class SearchDeviceImpl : public SearchDevice {
     cap_[which] = nc;
   }
 
-  uint32_t* log_reserve(uint64_t n) {
-    for (auto& c : log_)
-      if (c.cap - c.used >= n) {
-        uint32_t* p = c.ptr + c.used * RL::WORDS;
-        c.used += n;
-        return p;
-      }
+  void new_log_chunk(uint64_t min_cap) {
     LogChunk c;
-    c.cap = std::max<uint64_t>(n, 1u << 22);
+    c.cap = std::max<uint64_t>(min_cap, 1u << 22);
+    c.cap = std::min<uint64_t>(c.cap, 0xFFFFFFF0ull);
     c.ptr = dalloc<uint32_t>(c.cap * RL::WORDS);
-    c.used = n;
+    c.used = 0;
     log_.push_back(c);
-    return c.ptr;
   }
 
   static bool key_less(const std::vector<uint32_t>& a, uint32_t da, const std::vector<uint32_t>& b, uint32_t db) {
@@ -747,13 +837,20 @@ class SearchDeviceImpl : public SearchDevice {
   uint64_t cap_[2] = {0, 0};
   int cur_ = 0;
   uint64_t n_ = 0;
-  uint32_t* counters_ = nullptr;
+  static constexpr uint32_t kMaxBatch = 64;
+  uint32_t* ctr_ = nullptr;       // [kMaxBatch + 1][CTR_WORDS]: seed block + one per launch
+  uint32_t* glob_ = nullptr;      // witness count, flags
+  volatile uint32_t* hctr_ = nullptr;  // pinned host: [kMaxBatch][HC_WORDS] published counters, glob mirror
+  uint32_t* hctr_dev_ = nullptr;       // device view of hctr_
+  volatile uint32_t* glob_host_ = nullptr;
+  hipEvent_t ev_[kMaxBatch + 1] = {};
+  uint64_t stops_ = 0;
   unsigned long long* totals_ = nullptr;
   unsigned long long* best64_ = nullptr;
   unsigned long long* red_ = nullptr;
   uint32_t* keydev_ = nullptr;
   uint32_t* wit_ = nullptr;
-  uint32_t wit_cap_ = 0, wit_seen_ = 0;
+  uint32_t wit_cap_ = 0;
   std::vector<LogChunk> log_;
   size_t shm_ = 0, jit_shm_ = 0;
   int jit_smax_ = SMAX;

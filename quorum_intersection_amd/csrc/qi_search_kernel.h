@@ -215,19 +215,43 @@ struct WitLayout {
   static constexpr int WORDS = 2 * MW + 2 + ORDW;
 };
 
+// Per-launch counter block (CTR_WORDS words).  Launches are chained on the device: launch
+// k reads its input count, log position and stop state from launch k-1's block (or from a
+// host-written seed block), so the host enqueues launches without reading anything back
+// in between.  The atomically updated words and the plainly written ones sit on separate
+// 128-B lines.  The last block of a launch carries never-claimed input units over and
+// publishes the final block to pinned host memory (HC_* words), where the host polls it.
+enum : int {
+  C_OUT = 0,       // units written to units_out (spills + carried-over units)   [atomic]
+  C_HEAD = 1,      // dynamic claims past the statically assigned range           [atomic]
+  C_DONE = 2,      // used blocks that finished                                   [atomic]
+  C_NIN = 32,      // input units of this launch (the previous block's C_OUT)
+  C_LOGB = 33,     // first segment-log record of this launch
+  C_STOP = 34,     // 1: capacity would be exceeded; this launch (and the rest of the chain) did nothing
+  C_STATIC = 35,   // end of the statically assigned range (64 units per used block)
+  CTR_WORDS = 64,
+  HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_WORDS = 8
+};
+constexpr int TOT_SHARDS = 64;  // running totals: [TOT_SHARDS][16] u64, shard = block % 64
+
 struct SearchArgs {
   LocalDev f;
   const uint32_t* units_in;
-  uint32_t n_in;
   uint32_t* units_out;
   uint32_t out_cap;
-  uint32_t* counters;            // [0] out_count [1] head [2] wit_count [3] flags
-  uint32_t* records;             // [n_in][RecLayout::WORDS]
+  uint32_t log_cap;              // records in the current log chunk
+  const uint32_t* prev;          // previous launch's counter block (or the seed block)
+  uint32_t* counters;            // this launch's counter block
+  uint32_t* host_ctr;            // pinned host words HC_* for this launch (device pointer)
+  uint32_t* glob;                // [0] witness count [1] flags (whole batch)
+  uint32_t* records;             // log chunk base; this launch writes from prev's C_LOGB + C_NIN
   uint32_t* wit;
   uint32_t wit_cap;
-  unsigned long long* totals;    // nodes, evals, minq, zero_fallback, rounds, units_fetched
-  unsigned long long* best64;    // exact preorder key when MW == 1
-  uint32_t budget;
+  unsigned long long* totals;    // [TOT_SHARDS][16]: nodes, evals, minq, zero_fallback, rounds, units, ...
+  unsigned long long* best64;    // device-side best witness, best_pack(): exact when MW == 1,
+                                 // the first 64 path bits (conservative pruning) otherwise
+  uint32_t grow_budget;          // per-lane node budget while the frontier is below half the lanes
+  uint32_t run_budget;
   uint32_t grace;                // extra steps per lane once the unit queue is dry
   uint32_t evict_max;
   uint32_t half_m;
@@ -240,6 +264,15 @@ struct SearchArgs {
 };
 
 enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u };
+
+// 64-bit preorder summary of a node (path key K, depth d) for the device-side best key:
+// MW == 1: (K0, d) -- exact order; MW > 1: (K0, K1) -- "strictly greater" still implies
+// "strictly after in preorder", equal values are never pruned.
+template <int MW>
+__device__ __forceinline__ uint64_t best_pack(const uint32_t (&K)[MW], uint32_t d) {
+  if constexpr (MW == 1) return ((uint64_t)K[0] << 32) | d;
+  else return ((uint64_t)K[0] << 32) | K[1];
+}
 
 // preorder "strictly after" test of (K, d) vs (B, db): padded path bits, then depth.
 template <int MW>
@@ -321,6 +354,41 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 
   const uint32_t lane = threadIdx.x;
   const LocalDev& f = a.f;
+  // ---- chained launch prologue: input count, log position, capacity (wave-uniform) ----
+  const uint32_t* pc = a.prev;
+  uint32_t* cc = a.counters;
+  if (pc[C_STOP]) {  // an earlier launch of this chain stopped: the frontier stays where it is
+    if (blockIdx.x == 0 && lane == 0) {
+      cc[C_STOP] = 1u;
+      a.host_ctr[HC_STOP] = 1u;
+      a.host_ctr[HC_DONE] = 1u;
+    }
+    return;
+  }
+  const uint32_t n_in = pc[C_OUT];
+  const uint32_t log_base = pc[C_LOGB] + pc[C_NIN];
+  const uint32_t nb_used = min((n_in + (uint32_t)WAVE - 1u) / (uint32_t)WAVE, gridDim.x);
+  const uint32_t static_end = min(n_in, nb_used * (uint32_t)WAVE);
+  {
+    const uint64_t need_out = (uint64_t)n_in + (uint64_t)nb_used * WAVE * (uint64_t)(SMAX + 1 + a.evict_max);
+    const bool stop = need_out > (uint64_t)a.out_cap || (uint64_t)log_base + n_in > (uint64_t)a.log_cap;
+    if (blockIdx.x == 0 && lane == 0) {
+      cc[C_NIN] = n_in;
+      cc[C_LOGB] = log_base;
+      cc[C_STATIC] = static_end;
+      cc[C_STOP] = stop ? 1u : 0u;
+      if (stop || nb_used == 0) {  // nothing runs: publish now (else the last block does)
+        a.host_ctr[HC_OUT] = 0u;
+        a.host_ctr[HC_NIN] = n_in;
+        a.host_ctr[HC_LOGB] = log_base;
+        a.host_ctr[HC_STOP] = stop ? 1u : 0u;
+        a.host_ctr[HC_DONE] = 1u;
+      }
+    }
+    if (stop || blockIdx.x >= nb_used) return;
+  }
+  uint32_t* const records = a.records + (size_t)log_base * RL::WORDS;
+  const uint32_t budget = (n_in >= gridDim.x * (uint32_t)WAVE / 2u) ? a.run_budget : a.grow_budget;
 #define ST_(lvl, w) st[((lvl) * SE + (w)) * WAVE + lane]
 #define DOW_(w) dow[(w) * WAVE + lane]
 #define UR_(w, slot) uring[(w) * WAVE + (slot)]
@@ -336,7 +404,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   bool has = false, done = false;
   uint32_t nst = 0, sbase = 0;
   uint32_t steps = 0, evictions = 0;
-  uint32_t limit = a.budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
+  uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
   bool dry = false;
   uint32_t iter = 0;
   // current segment (one per fetched unit)
@@ -358,7 +426,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   bool ring_dead = false;
   uint64_t best64 = ~0ull;
   auto refill = [&](uint32_t base) {  // convergent: every lane stages one unit
-    const uint32_t cnt = min(a.n_in - base, (uint32_t)WAVE);
+    const uint32_t cnt = min(n_in - base, (uint32_t)WAVE);
     if (lane < cnt) {
       const uint4* src = (const uint4*)(a.units_in + (size_t)(base + lane) * UW);
 #pragma unroll
@@ -376,11 +444,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     ring_next = 0;
   };
   // the first 64 units of this block's range are statically assigned (no atomic)
-  if (blockIdx.x * WAVE < a.n_in) refill(blockIdx.x * WAVE);
+  if (blockIdx.x * WAVE < n_in) refill(blockIdx.x * WAVE);
   else ring_dead = true;
 
   auto close_segment = [&]() {
-    uint32_t* r = a.records + (size_t)seg_idx * RL::WORDS;
+    uint32_t* r = records + (size_t)seg_idx * RL::WORDS;
 #pragma unroll
     for (int w = 0; w < MW; ++w) r[w] = seg_K[w];
     r[MW] = seg_depth;
@@ -398,7 +466,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   auto pruned = [&](const uint32_t (&KK)[MW], uint32_t d) -> bool {
     bool p = false;
     if (a.has_best) p = after_key<MW>(KK, d, a.best_key, a.best_depth);
-    if (MW == 1) p = p || ((((uint64_t)KK[0] << 32) | d) > best64);
+    p = p || (best_pack<MW>(KK, d) > best64);
     return p;
   };
 
@@ -406,7 +474,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   auto write_unit = [&](uint32_t slot, const uint32_t (&UT)[MW], const uint32_t (&UD)[MW], const uint32_t (&UK)[MW],
                         uint32_t udepth, uint32_t ol, int extra_b) {
     if (slot >= a.out_cap) {
-      atomicOr(&a.counters[3], FLAG_OUT_OVERFLOW);
+      atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
       return;
     }
     uint32_t* u = a.units_out + (size_t)slot * UW;
@@ -510,9 +578,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (ring_next >= ring_cnt) {
         if (ring_dead) break;
         uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&a.counters[1], (uint32_t)WAVE);
+        if (lane == 0) base = static_end + atomicAdd(&cc[C_HEAD], (uint32_t)WAVE);
         base = __shfl(base, 0);
-        if (base >= a.n_in) {
+        if (base >= n_in) {
           ring_dead = true;
           break;
         }
@@ -560,12 +628,12 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       uint32_t h = 0;
       uint64_t b = ~0ull;
       if (lane == 0) {
-        h = __hip_atomic_load(&a.counters[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (MW == 1) b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h = static_end + __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       h = __shfl(h, 0);
       best64 = __shfl(b, 0);
-      if (!dry && (ring_dead || h >= a.n_in)) {
+      if (!dry && (ring_dead || h >= n_in)) {
         dry = true;
         limit = min(limit, steps + a.grace);
       }
@@ -578,7 +646,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (__any(spill)) {
         uint32_t total = 0;
         const uint32_t n = spill ? 1u + nst : 0u;
-        uint32_t slot = reserve(n, &a.counters[0], total);
+        uint32_t slot = reserve(n, &cc[C_OUT], total);
         if (spill) {
           write_unit(slot++, T, D, K, depth, dlen, -1);
           for (uint32_t i = nst; i > 0; --i) write_entry(slot++, (sbase + i - 1) & (SMAX - 1));
@@ -645,7 +713,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       const bool evict = push && nst == (uint32_t)SMAX;
       if (__any(evict)) {
         uint32_t total = 0;
-        const uint32_t slot = reserve(evict ? 1u : 0u, &a.counters[0], total);
+        const uint32_t slot = reserve(evict ? 1u : 0u, &cc[C_OUT], total);
         if (evict) {
           write_entry(slot, sbase & (SMAX - 1));
           sbase = (sbase + 1) & (SMAX - 1);
@@ -740,7 +808,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           seg_evals += 2u + dlen;  // cpp:184, |D| x cpp:192, visitor cpp:368
           ++seg_minq;
           if (vis_any) {  // disjoint quorum: witness, the unit ends here (cpp:369-377)
-            const uint32_t slot = atomicAdd(&a.counters[2], 1u);
+            const uint32_t slot = atomicAdd(&a.glob[0], 1u);
             if (slot < a.wit_cap) {
               uint32_t* wv = a.wit + (size_t)slot * WL::WORDS;
 #pragma unroll
@@ -752,9 +820,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
               wv[MW + 1] = dlen;
               for (uint32_t i = 0; i < (dlen + 3) / 4; ++i) wv[2 * MW + 2 + i] = DOW_(i);
             } else {
-              atomicOr(&a.counters[3], FLAG_WIT_OVERFLOW);
+              atomicOr(&a.glob[1], FLAG_WIT_OVERFLOW);
             }
-            if (MW == 1) atomicMin(a.best64, ((unsigned long long)K[0] << 32) | depth);
+            atomicMin(a.best64, (unsigned long long)best_pack<MW>(K, depth));
             nst = 0;  // everything left in this unit follows the witness in preorder
           }
         } else {  // not minimal: isMinimal stops at the first removable vertex in D order
@@ -776,18 +844,18 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     const uint32_t left = (ring_next < ring_cnt) ? ring_cnt - ring_next : 0u;
     if (left) {
       uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&a.counters[0], left);
+      if (lane == 0) base = atomicAdd(&cc[C_OUT], left);
       base = __shfl(base, 0);
       for (uint32_t i = lane; i < left; i += WAVE) {
         const uint32_t src = ring_pos + i, dst = base + i;
-        uint32_t* r = a.records + (size_t)src * RL::WORDS;
+        uint32_t* r = records + (size_t)src * RL::WORDS;
         for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
         if (dst < a.out_cap) {
           const uint4* s4 = (const uint4*)(a.units_in + (size_t)src * UW);
           uint4* d4 = (uint4*)(a.units_out + (size_t)dst * UW);
           for (int q = 0; q < UW / 4; ++q) d4[q] = s4[q];
         } else {
-          atomicOr(&a.counters[3], FLAG_OUT_OVERFLOW);
+          atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
         }
       }
     }
@@ -805,18 +873,61 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   tot_zfb = wsum(tot_zfb);
   const uint64_t tr = wsum((uint64_t)rounds);
   tot_fetched = wsum(tot_fetched);
-  if (lane == 0) {
-    atomicAdd(&a.totals[0], (unsigned long long)tot_nodes);
-    atomicAdd(&a.totals[1], (unsigned long long)tot_evals);
-    atomicAdd(&a.totals[2], (unsigned long long)tot_minq);
-    atomicAdd(&a.totals[3], (unsigned long long)tot_zfb);
-    atomicAdd(&a.totals[4], (unsigned long long)tr);
-    atomicAdd(&a.totals[5], (unsigned long long)tot_fetched);
-    atomicAdd(&a.totals[6], (unsigned long long)wave_iters);
-    atomicAdd(&a.totals[7], (unsigned long long)coop_phases);
+  if (lane == 0) {  // sharded: ~1800 waves per launch would otherwise queue on one L2 line
+    unsigned long long* tt = a.totals + (size_t)(blockIdx.x & (TOT_SHARDS - 1)) * 16;
+    atomicAdd(&tt[0], (unsigned long long)tot_nodes);
+    atomicAdd(&tt[1], (unsigned long long)tot_evals);
+    atomicAdd(&tt[2], (unsigned long long)tot_minq);
+    atomicAdd(&tt[3], (unsigned long long)tot_zfb);
+    atomicAdd(&tt[4], (unsigned long long)tr);
+    atomicAdd(&tt[5], (unsigned long long)tot_fetched);
+    atomicAdd(&tt[6], (unsigned long long)wave_iters);
+    atomicAdd(&tt[7], (unsigned long long)coop_phases);
 #ifdef QI_STAMPS
-    for (int q = 0; q < 6; ++q) atomicAdd(&a.totals[8 + q], (unsigned long long)stamp_sum[q]);
+    for (int q = 0; q < 6; ++q) atomicAdd(&tt[8 + q], (unsigned long long)stamp_sum[q]);
 #endif
+  }
+
+  // ---- last block of the launch: carry over never-claimed input units (whose waves all
+  // hit their budget before the queue ran dry) with zeroed records, publish the counters.
+  // Every counter read here is an atomic RMW, performed after the other blocks' returned
+  // atomics; nothing the other blocks stored plainly is read.
+  {
+    uint32_t old = 0;
+    if (lane == 0) old = atomicAdd(&cc[C_DONE], 1u);
+    old = __shfl(old, 0);
+    if (old == nb_used - 1u) {
+      uint32_t hd = 0, out = 0;
+      if (lane == 0) {
+        hd = atomicAdd(&cc[C_HEAD], 0u);
+        out = atomicAdd(&cc[C_OUT], 0u);
+      }
+      hd = __shfl(hd, 0);
+      out = __shfl(out, 0);
+      const uint32_t head = (uint32_t)min((uint64_t)static_end + hd, (uint64_t)n_in);
+      const uint32_t left = n_in - head;
+      for (uint32_t i = lane; i < left; i += WAVE) {
+        uint32_t* r = records + (size_t)(head + i) * RL::WORDS;
+        for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
+        const uint32_t dst = out + i;
+        if (dst < a.out_cap) {
+          const uint4* s4 = (const uint4*)(a.units_in + (size_t)(head + i) * UW);
+          uint4* d4 = (uint4*)(a.units_out + (size_t)dst * UW);
+          for (int q = 0; q < UW / 4; ++q) d4[q] = s4[q];
+        } else {
+          atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
+        }
+      }
+      if (lane == 0) {
+        out += left;
+        if (left) atomicExch(&cc[C_OUT], out);
+        a.host_ctr[HC_OUT] = out;
+        a.host_ctr[HC_NIN] = n_in;
+        a.host_ctr[HC_LOGB] = log_base;
+        a.host_ctr[HC_STOP] = 0u;
+        a.host_ctr[HC_DONE] = 1u;
+      }
+    }
   }
 #undef ST_
 #undef DOW_

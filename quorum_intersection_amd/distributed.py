@@ -1,14 +1,19 @@
 """Multi-GPU branch-and-bound search: one process per GPU, torch.distributed over RCCL.
 
 The search tree of iterateMinimalQuorums (quorum_intersection.cpp:252-346) is sharded
-by branch prefix: rank 0 starts from the root, and subtree units (branch prefixes) are
-handed to the other ranks as soon as its frontier grows; every rank then runs budgeted
-device launches on its own units.  Between launches the ranks exchange only
+by branch prefix:
 
-  * frontier sizes + best-witness keys   (one all_gather of a few int64s), and
-  * surplus units for rebalancing         (send/recv of packed unit bytes, host-planned),
+  1. rank 0 grows the frontier from the root (cpp:393) with a short chain of device
+     launches until it holds ``seed_units`` subtree units (branch prefixes);
+  2. it broadcasts those units (one RCCL broadcast of packed unit bytes), and every rank
+     keeps the strided share ``units[rank::world]`` -- neighbouring prefixes have
+     correlated subtree sizes, so a strided deal balances better than contiguous slices;
+  3. every rank runs chains of device launches on its own units; between chains the
+     ranks exchange only frontier sizes + best-witness keys (one all_gather of a few
+     int64s) and, when some rank would idle part of its GPU while another holds surplus,
+     move units with send/recv (host-planned, deterministic on every rank).
 
-so the data path has no collective.  Counts stay preorder-exact because every processed
+The data path has no collective.  Counts stay preorder-exact because every processed
 segment is logged with its root path key on the rank that processed it; at the end each
 rank reduces its log against the globally preorder-first witness and the totals are
 summed with one all_reduce.
@@ -41,8 +46,10 @@ class SearchBackend:
     def restart(self) -> None: ...
     def drop_log(self) -> None: ...
     def step(self) -> None: ...
+    def grow(self, target: int) -> None: ...
     def frontier(self) -> int: ...
     def keep_slice(self, begin: int, end: int) -> None: ...
+    def keep_strided(self, offset: int, stride: int) -> None: ...
     def export(self, count: int, dst: torch.Tensor) -> None: ...
     def import_(self, count: int, src: torch.Tensor) -> None: ...
     def local_best(self) -> Optional[Key]: ...
@@ -54,19 +61,21 @@ class SearchBackend:
 class DeviceSearch(SearchBackend):
     """C-ABI step-wise search (include/quorum_intersection.h) on one HIP device."""
 
-    def __init__(self, fbas, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0, jit: int = 0):
+    def __init__(self, fbas, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0, jit: int = 0,
+                 batch: int = 0):
         from . import _capi
         self._c = _capi
         self.L = _capi.lib()
         self.fbas = fbas
         h = ctypes.c_void_p()
-        opts = _capi.SearchOpts(grow_budget, run_budget, max_blocks, jit)
+        opts = _capi.SearchOpts(grow_budget, run_budget, max_blocks, jit, batch)
         _capi.check(self.L.qi_search_create(fbas.handle, ctypes.byref(opts), ctypes.byref(h)))
         self.h = h
         self.key_words = int(self.L.qi_search_key_words(h))
         self.unit_bytes = int(self.L.qi_search_unit_bytes(h))
         self.kernel_ms = 0.0
         self.launches = 0
+        self.data_device = torch.device("cuda", fbas.device)  # where exported units live
 
     def close(self):
         if self.h:
@@ -95,7 +104,7 @@ class DeviceSearch(SearchBackend):
         n = self.frontier()
         keep = None
         if n:
-            keep = torch.empty(n * self.unit_bytes, dtype=torch.uint8, device=f"cuda:{torch.cuda.current_device()}")
+            keep = torch.empty(n * self.unit_bytes, dtype=torch.uint8, device=self.data_device)
             self.export(n, keep)
         self._c.check(self.L.qi_search_restart(self.h))
         self.clear()
@@ -106,14 +115,23 @@ class DeviceSearch(SearchBackend):
         info = self._c.StepInfo()
         self._c.check(self.L.qi_search_step(self.h, ctypes.byref(info)))
         self.kernel_ms += info.kernel_ms
-        self.launches += 1
+        self.launches += int(info.launches)
         self.spec_launches = getattr(self, "spec_launches", 0) + int(info.specialized)
+
+    def grow(self, target):
+        info = self._c.StepInfo()
+        self._c.check(self.L.qi_search_grow(self.h, target, ctypes.byref(info)))
+        self.kernel_ms += info.kernel_ms
+        self.launches += int(info.launches)
 
     def frontier(self) -> int:
         return int(self.L.qi_search_frontier(self.h))
 
     def keep_slice(self, begin, end):
         self._c.check(self.L.qi_search_keep_slice(self.h, begin, end))
+
+    def keep_strided(self, offset, stride):
+        self._c.check(self.L.qi_search_keep_strided(self.h, offset, stride))
 
     def export(self, count, dst):
         self._c.check(self.L.qi_search_export(self.h, count, ctypes.c_void_p(dst.data_ptr())))
@@ -246,8 +264,17 @@ def _gather_state(be: SearchBackend, device, group) -> Tuple[List[int], List[Opt
     return sizes, keys
 
 
+def _unit_buf(be: SearchBackend, count: int, device) -> torch.Tensor:
+    return torch.empty(count * be.unit_bytes, dtype=torch.uint8, device=getattr(be, "data_device", device))
+
+
+def _to_comm(t: torch.Tensor, device) -> torch.Tensor:
+    """Unit bytes live on the backend's device; a CPU (gloo) group stages them on the host."""
+    return t if t.device == torch.device(device) else t.to(device)
+
+
 def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int = 1 << 17,
-                       rebalance: bool = True, min_move: int = 64) -> DistResult:
+                       rebalance: bool = True, min_move: int = 64, seed_units: int = 0) -> DistResult:
     """Run one full search across the ranks of `group`; every rank returns the result."""
     if dist.is_available() and dist.is_initialized():
         rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -256,13 +283,30 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
     t0 = time.perf_counter()
     be.restart()
     launches = 0
-    # (1) only rank 0 holds the root (cpp:393); the rebalancing below hands out units as
-    # soon as its frontier grows.  (Splitting a frontier every rank expanded "identically"
-    # would be unsound: the device spill order depends on atomics and differs per run.)
-    if rank != 0:
-        be.clear()
     moved = 0
-    # (2) independent launches; exchange sizes/best keys; rebalance surplus frontier
+    if world > 1:
+        # (1) rank 0 grows the frontier from the root (cpp:393) ...
+        target = seed_units or 2048 * world
+        if rank == 0:
+            be.grow(target)
+        n = torch.tensor([be.frontier() if rank == 0 else 0], dtype=torch.int64, device=device)
+        dist.broadcast(n, 0, group=group)
+        n = int(n.item())
+        # (2) ... hands it to every rank; each keeps the strided share units[rank::world]
+        if rank != 0:
+            be.clear()
+        if n:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            buf = _unit_buf(be, n, device)
+            if rank == 0:
+                be.export(n, buf)
+            cbuf = _to_comm(buf, device)
+            dist.broadcast(cbuf, src, group=group)
+            if cbuf is not buf:
+                buf.copy_(cbuf)
+            be.import_(n, buf)
+            be.keep_strided(rank, world)
+    # (3) independent chains of launches; exchange sizes/best keys; rebalance surplus
     while True:
         if be.frontier():
             be.step()
@@ -275,17 +319,21 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
             break
         if world > 1 and rebalance and needs_rebalance(sizes, lanes):
             for src, dst, cnt in plan_rebalance(sizes, min_move=min_move):
-                nbytes = cnt * be.unit_bytes
+                gsrc = dist.get_global_rank(group, src) if group is not None else src
+                gdst = dist.get_global_rank(group, dst) if group is not None else dst
                 if rank == src:
-                    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+                    buf = _unit_buf(be, cnt, device)
                     be.export(cnt, buf)
-                    dist.send(buf, dst, group=group)
+                    dist.send(_to_comm(buf, device), gdst, group=group)
                 elif rank == dst:
-                    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
-                    dist.recv(buf, src, group=group)
+                    buf = _unit_buf(be, cnt, device)
+                    cbuf = _to_comm(buf, device)
+                    dist.recv(cbuf, gsrc, group=group)
+                    if cbuf is not buf:
+                        buf.copy_(cbuf)
                     be.import_(cnt, buf)
                 moved += cnt
-    # (3) preorder-exact totals against the global best witness
+    # (4) preorder-exact totals against the global best witness
     sizes, keys = _gather_state(be, device, group) if world > 1 else ([0], [be.local_best()])
     best = best_of(keys)
     loc = be.reduce(best)

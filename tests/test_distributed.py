@@ -3,8 +3,9 @@
 A synthetic search backend replays the device engine's contract -- budgeted preorder
 walks of subtree units, stack spills, segment logs keyed by root path, pruning after the
 best witness -- over an irregular deterministic binary tree with planted witnesses, so
-the coordination (prefix split, best-key exchange, rebalancing by send/recv, exact
-preorder reduction) is checked against a sequential preorder walk.
+the coordination (frontier growth + broadcast + strided shares, best-key exchange,
+rebalancing by send/recv, exact preorder reduction) is checked against a sequential
+preorder walk.
 """
 import os
 import socket
@@ -98,6 +99,13 @@ class FakeSearch(SearchBackend):
     def keep_slice(self, b, e):
         self.units = self.units[b:e]
 
+    def keep_strided(self, offset, stride):
+        self.units = self.units[offset::stride]
+
+    def grow(self, target):
+        while self.units and len(self.units) < target:
+            self.step()
+
     def _pruned(self, k):
         return self.gbest is not None and _after(k, self.gbest)
 
@@ -185,11 +193,11 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = []
-        for salt, wit in TREES:
+        for (salt, wit), seed in [(tw, sd) for tw in TREES for sd in (0, 3, 40)]:
             t = Tree(salt, wit)
             be = FakeSearch(t, budget=3 + rank, max_units=5 + 3 * rank)
-            r = distributed_search(be, device="cpu", lanes=16, min_move=1)
-            res.append((salt, r.verdict, r.nodes, r.evals, r.q1, r.q2, r.moved_units))
+            r = distributed_search(be, device="cpu", lanes=16, min_move=1, seed_units=seed)
+            res.append((salt, seed, r.verdict, r.nodes, r.evals, r.q1, r.q2, r.moved_units))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -207,11 +215,11 @@ def test_distributed_gloo_world2_exact_counts():
         p.join(timeout=60)
         assert p.exitcode == 0
     moved = 0
-    for i, (salt, wit) in enumerate(TREES):
+    for i, ((salt, wit), seed) in enumerate([(tw, sd) for tw in TREES for sd in (0, 3, 40)]):
         nodes, evals, w = Tree(salt, wit).preorder()
         for rank in (0, 1):
-            s, verdict, n, e, q1, q2, mv = out[rank][i]
-            assert s == salt
+            s, sd, verdict, n, e, q1, q2, mv = out[rank][i]
+            assert (s, sd) == (salt, seed)
             assert verdict == (w is None)
             assert (n, e) == (nodes, evals), (salt, rank, n, e, nodes, evals)
             if w is not None:
