@@ -168,6 +168,9 @@ typedef struct {
   uint32_t roots;      /* distinct root TNs */
   uint32_t groups;     /* findBestNode column groups */
   uint32_t extra_terms;
+  uint32_t qmin_inside;  /* lower bound on a non-empty containsQuorum result, outside
+                            vertices unavailable (0 = no bound: threshold-0 sets) */
+  uint32_t qmin_outside; /* the same with outside vertices available (visitor, cpp:368) */
 } qi_shape;
 
 /* Compile (or load from the on-disk cache) the run-time specialised search kernel for

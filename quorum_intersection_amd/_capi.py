@@ -79,7 +79,7 @@ class StepInfo(ctypes.Structure):
 class Shape(ctypes.Structure):
     _fields_ = [("m", c_uint32), ("mask_words", c_uint32), ("tns", c_uint32), ("tn_words", c_uint32),
                 ("tns_with_children", c_uint32), ("roots", c_uint32), ("groups", c_uint32),
-                ("extra_terms", c_uint32)]
+                ("extra_terms", c_uint32), ("qmin_inside", c_uint32), ("qmin_outside", c_uint32)]
 
 
 class Totals(ctypes.Structure):

@@ -485,6 +485,8 @@ int qi_search_shape(const qi_search* s, qi_shape* out) {
   out->roots = L.R;
   out->groups = L.G;
   out->extra_terms = (uint32_t)L.extra_src.size();
+  out->qmin_inside = L.qmin[0];
+  out->qmin_outside = L.qmin[1];
   return QI_OK;
 }
 

@@ -352,7 +352,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_GRACE")) cfg_.grace = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
     jit_smax_ = SMAX;
-    if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(SMAX, std::atoi(e)));
+    if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
@@ -383,6 +383,8 @@ class SearchDeviceImpl : public SearchDevice {
     d_.R = f.R;
     d_.G = f.G;
     d_.m = f.m;
+    d_.qmin0 = f.qmin[0];
+    d_.qmin1 = f.qmin[1];
     keep(d_.tn = dupload(rec, stream_));
     keep(d_.extra_off = dupload(f.extra_off, stream_));
     keep(d_.extra_src = dupload(extra_src, stream_));
@@ -417,9 +419,9 @@ class SearchDeviceImpl : public SearchDevice {
     unsigned long long inf = ~0ull;
     HIP_CHECK(hipMemcpyAsync(best64_, &inf, 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
-    shm_ = (size_t)(SMAX * (MW + 1) * 64 + 2 * MW * 64 + UL::WORDS * 64 + ((UL::DMAX + 3) / 4) * 64) * 4;
+    shm_ = (size_t)dev::search_lds_words<MW, SMAX>() * 4;
     shm_ = (shm_ + 15) / 16 * 16;
-    jit_shm_ = (size_t)(jit_smax_ * (MW + 1) * 64 + 2 * MW * 64 + UL::WORDS * 64 + ((UL::DMAX + 3) / 4) * 64) * 4;
+    jit_shm_ = shm_ + (size_t)(jit_smax_ - SMAX) * (2 * MW + 1) * 64 * 4;  // QI_JIT_SMAX (diagnostics)
     jit_shm_ = (jit_shm_ + 15) / 16 * 16;
     HIP_CHECK(hipFuncSetAttribute((const void*)dev::search_kernel<MW, TW, SMAX>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
@@ -499,7 +501,7 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t D = std::max(1u, cfg_.lookahead);
     auto first_need = [&](uint64_t n) {
       const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
-      return n + nb * 64u * (smax + 1 + cfg_.evict_max);
+      return n + nb * 64u * (smax + 3 + cfg_.evict_max);  // search_body's need_out
     };
     {
       const uint64_t need = first_need(n_);
@@ -909,14 +911,14 @@ std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g) {
 bool jit_precompile(const LocalFlat& f, std::string* log) {
   const uint32_t mw = f.mw, tw = f.tw;
   int MW, TW, SMAX;
-  if (mw <= 1 && tw <= 1) { MW = 1; TW = 1; SMAX = 32; }
-  else if (mw <= 1 && tw <= 2) { MW = 1; TW = 2; SMAX = 32; }
-  else if (mw <= 1 && tw <= 4) { MW = 1; TW = 4; SMAX = 32; }
-  else if (mw <= 2 && tw <= 2) { MW = 2; TW = 2; SMAX = 32; }
-  else if (mw <= 2 && tw <= 4) { MW = 2; TW = 4; SMAX = 32; }
-  else if (mw <= 4 && tw <= 4) { MW = 4; TW = 4; SMAX = 16; }
-  else if (mw <= 4 && tw <= 8) { MW = 4; TW = 8; SMAX = 16; }
-  else if (mw <= 8 && tw <= 8) { MW = 8; TW = 8; SMAX = 16; }
+  if (mw <= 1 && tw <= 1) { MW = 1; TW = 1; SMAX = 24; }
+  else if (mw <= 1 && tw <= 2) { MW = 1; TW = 2; SMAX = 24; }
+  else if (mw <= 1 && tw <= 4) { MW = 1; TW = 4; SMAX = 24; }
+  else if (mw <= 2 && tw <= 2) { MW = 2; TW = 2; SMAX = 16; }
+  else if (mw <= 2 && tw <= 4) { MW = 2; TW = 4; SMAX = 16; }
+  else if (mw <= 4 && tw <= 4) { MW = 4; TW = 4; SMAX = 12; }
+  else if (mw <= 4 && tw <= 8) { MW = 4; TW = 8; SMAX = 12; }
+  else if (mw <= 8 && tw <= 8) { MW = 8; TW = 8; SMAX = 8; }
   else return false;
   if (!jit_eligible(f)) return false;
   return !jit_compile(jit_source(f, MW, TW, SMAX), log).empty();
@@ -924,14 +926,14 @@ bool jit_precompile(const LocalFlat& f, std::string* log) {
 
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg) {
   const uint32_t mw = f.mw, tw = f.tw;
-  if (mw <= 1 && tw <= 1) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 1, 32>(device, f, cfg));
-  if (mw <= 1 && tw <= 2) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 2, 32>(device, f, cfg));
-  if (mw <= 1 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 4, 32>(device, f, cfg));
-  if (mw <= 2 && tw <= 2) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<2, 2, 32>(device, f, cfg));
-  if (mw <= 2 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<2, 4, 32>(device, f, cfg));
-  if (mw <= 4 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<4, 4, 16>(device, f, cfg));
-  if (mw <= 4 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<4, 8, 16>(device, f, cfg));
-  if (mw <= 8 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<8, 8, 16>(device, f, cfg));
+  if (mw <= 1 && tw <= 1) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 1, 24>(device, f, cfg));
+  if (mw <= 1 && tw <= 2) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 2, 24>(device, f, cfg));
+  if (mw <= 1 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 4, 24>(device, f, cfg));
+  if (mw <= 2 && tw <= 2) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<2, 2, 16>(device, f, cfg));
+  if (mw <= 2 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<2, 4, 16>(device, f, cfg));
+  if (mw <= 4 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<4, 4, 12>(device, f, cfg));
+  if (mw <= 4 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<4, 8, 12>(device, f, cfg));
+  if (mw <= 8 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<8, 8, 8>(device, f, cfg));
   throw Error(QI_ERR_UNSUPPORTED, "searched SCC too large for the device kernels (|SCC| > 256 or > 256 TNs)");
 }
 

@@ -250,6 +250,84 @@ std::vector<std::vector<uint32_t>> planes(const std::vector<uint32_t>& sorted, u
 
 }  // namespace
 
+// Lower bound on the number of SCC vertices in any set that satisfies a TN (cpp:90-138
+// with monotone thresholds), per polarity.  Items of a TN are its validator refs (points =
+// multiplicity, cost 1) and its inner sets (points = multiplicity, cost = their bound).
+// When the vertex supports of the items are pairwise disjoint, costs add and the bound is
+// the exact minimum-cost cover of `threshold` points (0/1 knapsack over points); when they
+// overlap, only "one item must be satisfied" is used.  The minimum over the SCC's roots
+// bounds every non-empty greatest fixpoint from below.
+uint32_t min_quorum_size(const LocalFlat& L, int pol) {
+  constexpr uint32_t INF = 0xFFFFFFFFu;
+  const uint32_t T = L.T, mw = L.mw, tw = L.tw;
+  std::vector<uint32_t> cost(T, INF);
+  std::vector<std::vector<uint32_t>> sup(T, std::vector<uint32_t>(mw, 0u));
+  for (uint32_t t = 0; t < T; ++t) {  // children-first order
+    // multiplicities from plane 0 + extra planes
+    std::vector<uint32_t> vm(L.m, 0), cm(T, 0);
+    for (uint32_t v = 0; v < L.m; ++v)
+      if ((L.vmask[(size_t)t * mw + (v >> 5)] >> (v & 31)) & 1u) ++vm[v];
+    for (uint32_t c = 0; c < T; ++c)
+      if ((L.cmask[(size_t)t * tw + (c >> 5)] >> (c & 31)) & 1u) ++cm[c];
+    for (uint32_t e = L.extra_off[t]; e < L.extra_off[t + 1]; ++e) {
+      const uint32_t src = L.extra_src[e], msk = L.extra_mask[e];
+      for (uint32_t b = 0; b < 32; ++b) {
+        if (!((msk >> b) & 1u)) continue;
+        if (src < mw) ++vm[src * 32 + b];
+        else ++cm[(src - mw) * 32 + b];
+      }
+    }
+    struct Item { uint32_t pts, cost; };
+    std::vector<Item> items;
+    bool disjoint = true;
+    std::vector<uint32_t> acc(mw, 0u);
+    auto add_support = [&](const std::vector<uint32_t>& s) {
+      for (uint32_t w = 0; w < mw; ++w) {
+        if (acc[w] & s[w]) disjoint = false;
+        acc[w] |= s[w];
+      }
+    };
+    for (uint32_t v = 0; v < L.m; ++v)
+      if (vm[v]) {
+        items.push_back({vm[v], 1u});
+        std::vector<uint32_t> one(mw, 0u);
+        one[v >> 5] = 1u << (v & 31);
+        add_support(one);
+      }
+    for (uint32_t c = 0; c < T; ++c)
+      if (cm[c]) {
+        if (cost[c] != INF) items.push_back({cm[c], cost[c]});
+        add_support(sup[c]);
+      }
+    sup[t] = acc;
+    const int32_t th = L.thr[2 * t + pol];
+    if (L.flags[t] & 1u) {
+      cost[t] = 0;
+    } else if (th <= 0) {
+      cost[t] = 0;
+    } else if (th == INT32_MAX) {
+      cost[t] = INF;
+    } else if (disjoint) {
+      std::vector<uint64_t> dp((size_t)th + 1, INF);
+      dp[0] = 0;
+      for (const Item& it : items)
+        for (int32_t p = th; p >= 0; --p) {
+          if (dp[p] == INF) continue;
+          const int32_t q = std::min<int32_t>(th, p + (int32_t)it.pts);
+          dp[q] = std::min<uint64_t>(dp[q], dp[p] + it.cost);
+        }
+      cost[t] = dp[th] >= INF ? INF : (uint32_t)dp[th];
+    } else {
+      uint32_t lo = INF;
+      for (const Item& it : items) lo = std::min(lo, it.cost);
+      cost[t] = lo;
+    }
+  }
+  uint32_t q = INF;
+  for (uint32_t r = 0; r < L.R; ++r) q = std::min(q, cost[L.root_tn[r]]);
+  return std::min(q, L.m + 1);  // no satisfiable root: every fixpoint is empty
+}
+
 LocalFlat flatten_local(const Graph& g, const std::vector<uint32_t>& scc) {
   LocalFlat L;
   L.m = (uint32_t)scc.size();
@@ -413,6 +491,9 @@ LocalFlat flatten_local(const Graph& g, const std::vector<uint32_t>& scc) {
     for (size_t q = 1; q < p.size(); ++q)
       for (uint32_t w = 0; w < L.mw; ++w) L.grp_extra.push_back(p[q][w]);
     L.grp_extra_off[gi + 1] = L.grp_extra_off[gi] + (uint32_t)(p.size() > 1 ? p.size() - 1 : 0);
+  }
+  if (!L.nonmonotone) {
+    for (int pol = 0; pol < 2; ++pol) L.qmin[pol] = min_quorum_size(L, pol);
   }
   return L;
 }

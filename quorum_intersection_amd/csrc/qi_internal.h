@@ -121,6 +121,11 @@ struct LocalFlat {
   std::vector<uint32_t> grp_col;    // [G][mw] in-edge sources, multiplicity plane 0
   std::vector<uint32_t> grp_extra_off;  // [G+1] extra multiplicity planes (mw words each)
   std::vector<uint32_t> grp_extra;
+  // Smallest possible non-empty greatest fixpoint, per polarity (outside unavailable /
+  // available): every survivor y needs the internal vertices of one of its slices, so
+  // containsQuorum(X) is empty whenever |X| < qmin.  0 disables the test (threshold-0
+  // sets make the slice predicate non-monotone).
+  uint32_t qmin[2] = {0, 0};
 };
 LocalFlat flatten_local(const Graph& g, const std::vector<uint32_t>& scc);
 

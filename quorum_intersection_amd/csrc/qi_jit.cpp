@@ -66,12 +66,34 @@ bool jit_eligible(const LocalFlat& f) {
 std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps) {
   std::ostringstream o;
   if (stamps) o << "#define QI_STAMPS 1\n";
+  // diagnostics only (never set for measurements): QI_JIT_DEFINES="A,B=2" adds #defines,
+  // e.g. the QI_ABL_* ablations of qi_search_kernel.h that repeat one section
+  if (const char* e = std::getenv("QI_JIT_DEFINES")) {
+    std::string d = e;
+    size_t p = 0;
+    while (p < d.size()) {
+      size_t q = d.find(',', p);
+      if (q == std::string::npos) q = d.size();
+      std::string item = d.substr(p, q - p);
+      const size_t eq = item.find('=');
+      if (!item.empty()) o << "#define " << (eq == std::string::npos ? item + " 1" : item.substr(0, eq) + " " + item.substr(eq + 1)) << "\n";
+      p = q + 1;
+    }
+  }
   o << kSearchKernelSrc << "\nnamespace qi {\nnamespace dev {\n";
   o << "// generated evaluator: m=" << f.m << " T=" << f.T << " R=" << f.R << " G=" << f.G << "\n";
   o << "struct SpecEval {\n";
   // ---------------- containsQuorum ----------------
   o << "  template <int POL>\n  static __device__ __forceinline__ bool gfp(const LocalDev&, uint32_t (&X)[" << MW
-    << "], uint32_t pol, uint32_t& rounds) {\n    (void)pol;\n    for (;;) {\n      if (!(X[0]";
+    << "], uint32_t pol, uint32_t& rounds) {\n    (void)pol;\n";
+  // |X| < qmin => empty fixpoint (LocalFlat::qmin), before any round
+  o << "    { const uint32_t c = __popc(X[0])";
+  for (int w = 1; w < MW; ++w) o << " + __popc(X[" << w << "])";
+  o << "; const uint32_t q = POL == 0 ? " << f.qmin[0] << "u : (POL == 1 ? " << f.qmin[1] << "u : (pol ? " << f.qmin[1]
+    << "u : " << f.qmin[0] << "u));\n      if (c < q) {";
+  for (int w = 0; w < MW; ++w) o << " X[" << w << "] = 0u;";
+  o << " } }\n";
+  o << "    for (;;) {\n      if (!(X[0]";
   for (int w = 1; w < MW; ++w) o << " | X[" << w << "]";
   o << ")) return false;\n      ++rounds;\n";
   for (int w = 0; w < TW; ++w) o << "      uint32_t sb" << w << " = 0u;\n";
@@ -163,6 +185,9 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
 }
 
 std::vector<char> jit_compile(const std::string& src, std::string* log) {
+  if (const char* d = std::getenv("QI_JIT_DUMP")) {  // diagnostics: keep the generated source
+    std::ofstream(d) << src;
+  }
   const std::string dir = cache_dir();
   char key[32];
   std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v1"));

@@ -52,6 +52,7 @@ struct LocalDev {
   const uint32_t* grp_extra_off;  // [G+1]
   const uint32_t* grp_extra;      // [E][MW]
   uint32_t T, R, G, m;
+  uint32_t qmin0, qmin1;       // LocalFlat::qmin: |X| below it => empty fixpoint
 };
 
 // Wave-uniform tables are read through the constant address space so the compiler emits
@@ -66,7 +67,12 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 __device__ __forceinline__ uint32_t rank_in(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
-__device__ __forceinline__ uint32_t bcast0(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+// Lane 0's value, wave-uniform: v_readlane (a __shfl from lane 0 is an LDS ds_bpermute
+// round trip).
+__device__ __forceinline__ uint32_t lane0(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 0); }
+__device__ __forceinline__ uint64_t lane0(uint64_t v) {
+  return ((uint64_t)lane0((uint32_t)(v >> 32)) << 32) | lane0((uint32_t)v);
+}
 
 template <int MW, int TW>
 __device__ __forceinline__ uint32_t extra_terms(const LocalDev& f, uint32_t t, const uint32_t (&X)[MW],
@@ -94,6 +100,16 @@ __device__ __forceinline__ uint32_t extra_terms(const LocalDev& f, uint32_t t, c
 template <int MW, int TW, int POL>
 __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32_t pol, uint32_t& rounds) {
   using R = TnRec<MW, TW>;
+  {  // a non-empty fixpoint needs >= qmin vertices (LocalFlat::qmin): skip the rounds
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < MW; ++w) c += __popc(X[w]);
+    const uint32_t q = POL == 0 ? f.qmin0 : (POL == 1 ? f.qmin1 : (pol ? f.qmin1 : f.qmin0));
+    if (c < q) {
+#pragma unroll
+      for (int w = 0; w < MW; ++w) X[w] = 0u;
+    }
+  }
   for (;;) {
     uint32_t any = 0;
 #pragma unroll
@@ -261,6 +277,7 @@ struct SearchArgs {
   uint32_t best_depth;
   uint32_t best_key[8];
   uint32_t scc_mask[8];
+  uint32_t diag;                 // 0; opaque to the compiler (keeps QI_ABL_* repeats alive)
 };
 
 enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u };
@@ -299,21 +316,32 @@ __device__ __forceinline__ void key_prefix_bit(uint32_t (&K)[MW], uint32_t de) {
   }
 }
 
-// Wave-aggregated reservation of n (per lane) slots on a global counter.
+// Wave-aggregated reservation of n (per lane, n < 2^NB) slots on a global counter: the
+// exclusive wave prefix sum is bit-sliced over NB ballots (mbcnt per bit plane), so it
+// needs no LDS round trips; one atomic per wave.  Convergent.
+template <int NB>
 __device__ __forceinline__ uint32_t reserve(uint32_t n, uint32_t* counter, uint32_t& total_out) {
-  const uint32_t lane = lane_id();
-  uint32_t x = n;
+  uint32_t pre = 0, total = 0;
 #pragma unroll
-  for (int d = 1; d < WAVE; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d);
-    if ((int)lane >= d) x += y;
+  for (int b = 0; b < NB; ++b) {
+    const uint64_t m = __ballot((n >> b) & 1u);
+    pre += rank_in(m) << b;
+    total += (uint32_t)__popcll(m) << b;
   }
-  const uint32_t total = __shfl(x, WAVE - 1);
   uint32_t base = 0;
-  if (lane == 0 && total) base = atomicAdd(counter, total);
-  base = __shfl(base, 0);
+  if (lane_id() == 0 && total) base = atomicAdd(counter, total);
+  base = lane0(base);
   total_out = total;
-  return base + x - n;
+  return base + pre;
+}
+
+// LDS words of one search wavefront (search_body's carve-up below).
+template <int MW, int SMAX>
+constexpr int search_lds_words() {
+  return SMAX * (2 * MW + 1) * WAVE             // DFS stack below the top entry
+         + 2 * MW * WAVE                        // co_NE, co_VIS
+         + (MW + 1) * WAVE                      // co_D, co_OWN
+         + ((UnitLayout<MW>::DMAX + 3) / 4) * WAVE;  // D order
 }
 
 // Diagnostic build only (QI_STAMPS, run-time specialised kernel with jit=3): per-wave
@@ -328,10 +356,17 @@ __device__ __forceinline__ uint32_t reserve(uint32_t n, uint32_t* counter, uint3
     stamp_sum[(slot)] += now_ - stamp_prev;                              \
     stamp_prev = now_;                                                   \
   } while (0)
+#elif defined(QI_MARKS)
+// diagnostics: assembly markers at the section boundaries (static instruction counts)
+#define QI_STAMP(slot) asm volatile(";QIMARK " #slot ::: "memory")
 #else
 #define QI_STAMP(slot) \
   do {                 \
   } while (0)
+#endif
+
+#ifndef QI_INSTALL_AGE
+#define QI_INSTALL_AGE 0
 #endif
 
 template <int MW, int TW, int SMAX, class EV>
@@ -341,16 +376,21 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   using WL = WitLayout<MW>;
   constexpr int DMAX = UL::DMAX;
   constexpr int UW = UL::WORDS;
-  constexpr int SE = MW + 1;  // stack entry words: T'[MW], packed(b, depth, dlen)
-
+  // stack entry: T' [MW] | D of the inclusion child [MW] | packed (b, depth, |D| before b)
+  constexpr int SE = 2 * MW + 1;
+  constexpr int RB = (SMAX + 3 < 64) ? 6 : (SMAX + 3 < 128 ? 7 : 8);  // bits of a lane's spill count
   constexpr int OW = (DMAX + 3) / 4;  // packed D-order words (4 vertex bytes each)
-  (void)OW;
+  // the next unit is loaded into registers one node ahead (small units); large units are
+  // loaded when installed
+  constexpr bool PREFETCH = UW <= 20;
+  constexpr int FW = PREFETCH ? UW : 4;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* st = lds;                                          // [SMAX][SE][64]
   uint32_t* co_NE = st + SMAX * SE * WAVE;                      // [MW][64] per pending rank
   uint32_t* co_VIS = co_NE + MW * WAVE;                         // [MW][64] per pending rank
-  uint32_t* uring = co_VIS + MW * WAVE;                         // [UW][64] staged units
-  uint32_t* dow = uring + UW * WAVE;                            // [OW][64] D in branch order
+  uint32_t* co_D = co_VIS + MW * WAVE;                          // [MW][64] pending owners' D
+  uint32_t* co_OWN = co_D + MW * WAVE;                          // [64] owner lane | dlen << 8
+  uint32_t* dow = co_OWN + WAVE;                                // [OW][64] D in branch order
 
   const uint32_t lane = threadIdx.x;
   const LocalDev& f = a.f;
@@ -370,7 +410,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   const uint32_t nb_used = min((n_in + (uint32_t)WAVE - 1u) / (uint32_t)WAVE, gridDim.x);
   const uint32_t static_end = min(n_in, nb_used * (uint32_t)WAVE);
   {
-    const uint64_t need_out = (uint64_t)n_in + (uint64_t)nb_used * WAVE * (uint64_t)(SMAX + 1 + a.evict_max);
+    // per lane at most: current node + top of stack + SMAX entries + a prefetched unit
+    // spilled once, plus evict_max evictions
+    const uint64_t need_out = (uint64_t)n_in + (uint64_t)nb_used * WAVE * (uint64_t)(SMAX + 3 + a.evict_max);
     const bool stop = need_out > (uint64_t)a.out_cap || (uint64_t)log_base + n_in > (uint64_t)a.log_cap;
     if (blockIdx.x == 0 && lane == 0) {
       cc[C_NIN] = n_in;
@@ -391,23 +433,40 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   const uint32_t budget = (n_in >= gridDim.x * (uint32_t)WAVE / 2u) ? a.run_budget : a.grow_budget;
 #define ST_(lvl, w) st[((lvl) * SE + (w)) * WAVE + lane]
 #define DOW_(w) dow[(w) * WAVE + lane]
-#define UR_(w, slot) uring[(w) * WAVE + (slot)]
   // byte i of this lane's D order (ds_write_b8 into the packed word)
   auto set_ord = [&](uint32_t i, uint32_t v) {
     ((uint8_t*)dow)[(((i >> 2) * WAVE + lane) << 2) + (i & 3u)] = (uint8_t)v;
   };
 
+  // current node
   uint32_t T[MW], D[MW], K[MW];
 #pragma unroll
   for (int w = 0; w < MW; ++w) T[w] = D[w] = K[w] = 0;
   uint32_t depth = 0, dlen = 0;
   bool has = false, done = false;
-  uint32_t nst = 0, sbase = 0;
+  // top of the DFS stack in registers; `nst` entries below it in LDS (circular from sbase_)
+  uint32_t tT[MW], tD[MW], tpk = 0;
+#pragma unroll
+  for (int w = 0; w < MW; ++w) tT[w] = tD[w] = 0;
+  bool tvalid = false;
+  uint32_t nst = 0, sbase_ = 0;
+  auto spos = [&](uint32_t i) -> uint32_t {  // circular stack position of entry i (0 = bottom)
+    const uint32_t p = sbase_ + i;
+    return p >= (uint32_t)SMAX ? p - (uint32_t)SMAX : p;
+  };
   uint32_t steps = 0, evictions = 0;
   uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
-  bool dry = false;
+  bool dry = false;         // wave-uniform: no unit left to claim (head >= n_in)
   uint32_t iter = 0;
-  // current segment (one per fetched unit)
+  // the next unit of this lane: claimed index + (PREFETCH) its words in registers
+  // A unit claimed at the end of iteration i is installed at the start of iteration
+  // i + 1 + QI_INSTALL_AGE (diagnostics; 0 measured best).
+  bool fpend = false;
+  uint32_t fidx = 0, fage = 1;
+  uint32_t fdat[FW];
+#pragma unroll
+  for (int q = 0; q < FW; ++q) fdat[q] = 0;
+  // current segment (one per installed unit)
   bool seg_open = false;
   uint32_t seg_idx = 0, seg_depth = 0, seg_count = 0, seg_evals = 0, seg_minq = 0, seg_zfb = 0;
   uint32_t seg_K[MW];
@@ -420,42 +479,62 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint64_t stamp_sum[6] = {0, 0, 0, 0, 0, 0};
   uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
 #endif
-
-  // wave-uniform LDS ring of staged units (see (2) below)
-  uint32_t ring_src = 0, ring_cnt = 0, ring_next = 0;
-  bool ring_dead = false;
   uint64_t best64 = ~0ull;
-  auto refill = [&](uint32_t base) {  // convergent: every lane stages one unit
-    const uint32_t cnt = min(n_in - base, (uint32_t)WAVE);
-    if (lane < cnt) {
-      const uint4* src = (const uint4*)(a.units_in + (size_t)(base + lane) * UW);
+
+  auto load_unit = [&](uint32_t idx) {  // issue the loads (consumed at install)
+    if constexpr (PREFETCH) {
+      const uint4* src = (const uint4*)(a.units_in + (size_t)idx * UW);
 #pragma unroll
       for (int q = 0; q < UW / 4; ++q) {
         const uint4 v = src[q];
-        UR_(4 * q + 0, lane) = v.x;
-        UR_(4 * q + 1, lane) = v.y;
-        UR_(4 * q + 2, lane) = v.z;
-        UR_(4 * q + 3, lane) = v.w;
+        fdat[4 * q + 0] = v.x;
+        fdat[4 * q + 1] = v.y;
+        fdat[4 * q + 2] = v.z;
+        fdat[4 * q + 3] = v.w;
       }
     }
-    __syncthreads();
-    ring_src = base;
-    ring_cnt = cnt;
-    ring_next = 0;
   };
-  // the first 64 units of this block's range are statically assigned (no atomic)
-  if (blockIdx.x * WAVE < n_in) refill(blockIdx.x * WAVE);
-  else ring_dead = true;
+  auto unit_word = [&](int wi) -> uint32_t {  // word wi of the claimed unit
+    if constexpr (PREFETCH) return fdat[wi];
+    else return a.units_in[(size_t)fidx * UW + wi];
+  };
+  // the statically assigned first unit of this lane (no atomic)
+  if (blockIdx.x * WAVE + lane < n_in) {
+    fidx = blockIdx.x * WAVE + lane;
+    fpend = true;
+    load_unit(fidx);
+  }
+  uint32_t pool_next = 0, pool_end = 0;  // wave-uniform pool of claimed unit indices
+  bool pool_dead = static_end >= n_in;
 
-  auto close_segment = [&]() {
-    uint32_t* r = records + (size_t)seg_idx * RL::WORDS;
+  // A closed segment's record is written at the end of the iteration (flush_record), not
+  // where the segment closes: a store just before the next unit's install would make
+  // the install's wait for its prefetched loads also wait for the store.
+  bool rec_pend = false;
+  uint32_t rec[RL::WORDS], rec_idx = 0;
 #pragma unroll
-    for (int w = 0; w < MW; ++w) r[w] = seg_K[w];
-    r[MW] = seg_depth;
-    r[MW + 1] = seg_count;
-    r[MW + 2] = seg_evals;
-    r[MW + 3] = seg_minq;
-    r[MW + 4] = seg_zfb;
+  for (int w = 0; w < RL::WORDS; ++w) rec[w] = 0;
+  auto flush_record = [&]() {
+    if (rec_pend) {
+#ifndef QI_ABL_NOREC  // diagnostics: no record stores (counts then only via running totals)
+      uint32_t* r = records + (size_t)rec_idx * RL::WORDS;
+#pragma unroll
+      for (int w = 0; w < RL::WORDS; ++w) r[w] = rec[w];
+#endif
+      rec_pend = false;
+    }
+  };
+  auto close_segment = [&]() {
+    flush_record();
+#pragma unroll
+    for (int w = 0; w < MW; ++w) rec[w] = seg_K[w];
+    rec[MW] = seg_depth;
+    rec[MW + 1] = seg_count;
+    rec[MW + 2] = seg_evals;
+    rec[MW + 3] = seg_minq;
+    rec[MW + 4] = seg_zfb;
+    rec_idx = seg_idx;
+    rec_pend = true;
     tot_nodes += seg_count;
     tot_evals += seg_evals;
     tot_minq += seg_minq;
@@ -470,7 +549,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     return p;
   };
 
-  // write one unit (T, D given as masks, order = dord[0..ol) + optional extra byte)
+  // write one unit (T, D given as masks, order = DOW[0..ol) + optional extra byte)
   auto write_unit = [&](uint32_t slot, const uint32_t (&UT)[MW], const uint32_t (&UD)[MW], const uint32_t (&UK)[MW],
                         uint32_t udepth, uint32_t ol, int extra_b) {
     if (slot >= a.out_cap) {
@@ -496,167 +575,160 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       u[UL::ORD + i] = word;
     }
   };
-
-  // write stack entry at circular position pos as a unit
-  auto write_entry = [&](uint32_t slot, uint32_t pos) {
-    uint32_t UT[MW], UD[MW], UK[MW];
+  // a stack entry (T', D', packed) as a unit: the inclusion child it stands for
+  auto write_entry = [&](uint32_t slot, const uint32_t (&ET)[MW], const uint32_t (&ED)[MW], uint32_t pk) {
+    uint32_t UK[MW];
+#pragma unroll
+    for (int w = 0; w < MW; ++w) UK[w] = K[w];
+    const uint32_t b = pk & 255u, de = (pk >> 8) & 511u, dle = pk >> 17;
+    key_prefix_bit<MW>(UK, de);
+    write_unit(slot, ET, ED, UK, de + 1, dle, (int)b);
+  };
+  auto write_lds_entry = [&](uint32_t slot, uint32_t pos) {
+    uint32_t ET[MW], ED[MW];
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
-      UT[w] = ST_(pos, w);
-      UD[w] = 0;
-      UK[w] = K[w];
+      ET[w] = ST_(pos, w);
+      ED[w] = ST_(pos, MW + w);
     }
-    const uint32_t pk = ST_(pos, MW);
-    const uint32_t b = pk & 255u, de = (pk >> 8) & 511u, dle = pk >> 17;
-    for (uint32_t i = 0; i < (dle + 3) / 4; ++i) {
-      const uint32_t word = DOW_(i);
+    write_entry(slot, ET, ED, ST_(pos, 2 * MW));
+  };
+  // a claimed but not installed unit goes back out unchanged, its record zeroed
+  auto write_claimed = [&](uint32_t slot) {
+    uint32_t* r = records + (size_t)fidx * RL::WORDS;
 #pragma unroll
-      for (uint32_t j = 0; j < 4; ++j)
-        if (i * 4 + j < dle) {
-          const uint32_t v = (word >> (8 * j)) & 255u;
-          UD[v >> 5] |= 1u << (v & 31u);
-        }
+    for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
+    if (slot >= a.out_cap) {
+      atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
+      return;
     }
-    UD[b >> 5] |= 1u << (b & 31u);
-    key_prefix_bit<MW>(UK, de);
-    write_unit(slot, UT, UD, UK, de + 1, dle, (int)b);
+    uint32_t* u = a.units_out + (size_t)slot * UW;
+#pragma unroll
+    for (int q = 0; q < UW; ++q) u[q] = unit_word(q);
   };
 
   for (;;) {
-    // ---- (1) continue the current unit from its stack -------------------------------
+    // ---- (1) lanes without a node: pop the top of stack, else install the next unit ----
     if (!done && !has) {
-      while (nst > 0) {
-        --nst;
-        const uint32_t pos = (sbase + nst) & (SMAX - 1);
-        const uint32_t pk = ST_(pos, MW);
-        const uint32_t b = pk & 255u, de = (pk >> 8) & 511u, dle = pk >> 17;
+      if (tvalid) {
+        const uint32_t b = tpk & 255u, de = (tpk >> 8) & 511u, dle = tpk >> 17;
         uint32_t NK[MW];
 #pragma unroll
         for (int w = 0; w < MW; ++w) NK[w] = K[w];
         key_prefix_bit<MW>(NK, de);
         if (pruned(NK, de + 1)) {  // deeper entries precede shallower ones: drop all
+          tvalid = false;
           nst = 0;
-          break;
-        }
-        for (uint32_t i = dle >> 2; i < (dlen + 3) / 4; ++i) {  // drop inclusions below `de`
-          const uint32_t word = DOW_(i);
+        } else {
 #pragma unroll
-          for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t p = i * 4 + j;
-            if (p >= dle && p < dlen) {
-              const uint32_t v = (word >> (8 * j)) & 255u;
-              D[v >> 5] &= ~(1u << (v & 31u));
+          for (int w = 0; w < MW; ++w) {
+            T[w] = tT[w];
+            D[w] = tD[w];
+            K[w] = NK[w];
+          }
+          set_ord(dle, b);
+          dlen = dle + 1;
+          depth = de + 1;
+          has = true;
+          if (nst > 0) {  // refill the top from LDS; first used at the next pop
+            --nst;
+            const uint32_t pos = spos(nst);
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+              tT[w] = ST_(pos, w);
+              tD[w] = ST_(pos, MW + w);
             }
+            tpk = ST_(pos, 2 * MW);
+          } else {
+            tvalid = false;
           }
         }
-        D[b >> 5] |= 1u << (b & 31u);
-        set_ord(dle, b);
-        dlen = dle + 1;
-#pragma unroll
-        for (int w = 0; w < MW; ++w) {
-          T[w] = ST_(pos, w);
-          K[w] = NK[w];
-        }
-        depth = de + 1;
-        has = true;
-        break;
       }
-      if (!has && nst == 0) {
-        if (seg_open) close_segment();
-        if (steps >= limit) done = true;
+      if (!has) {
+        if (seg_open) close_segment();  // the unit's subtree is done
+        if (fpend && fage >= QI_INSTALL_AGE && steps < limit) {  // install the claimed unit
+          uint32_t UK[MW];
+#pragma unroll
+          for (int w = 0; w < MW; ++w) {
+            T[w] = unit_word(UL::T_ + w);
+            D[w] = unit_word(UL::D_ + w);
+            UK[w] = unit_word(UL::K_ + w);
+          }
+          const uint32_t ud = unit_word(UL::DEPTH);
+          dlen = unit_word(UL::DLEN);
+          const uint32_t nw = (dlen + 3) / 4;
+          if constexpr (OW <= 8) {
+#pragma unroll
+            for (int i = 0; i < OW; ++i)
+              if ((uint32_t)i < nw) DOW_(i) = unit_word(UL::ORD + i);
+          } else {
+            for (uint32_t i = 0; i < nw; ++i) DOW_(i) = unit_word(UL::ORD + (int)i);
+          }
+          fpend = false;
+          ++tot_fetched;
+          seg_idx = fidx;
+          seg_open = true;
+          seg_count = seg_evals = seg_minq = seg_zfb = 0;
+#pragma unroll
+          for (int w = 0; w < MW; ++w) seg_K[w] = K[w] = UK[w];
+          seg_depth = depth = ud;
+          nst = 0;
+          sbase_ = 0;
+          tvalid = false;
+          if (pruned(UK, ud)) close_segment();  // zero record
+          else has = true;
+        }
       }
     }
 
-    QI_STAMP(0);  // pop / segment close
-    // ---- (2) fetch new units from the wave's LDS ring --------------------------------
-    // The ring holds up to 64 units staged by one coalesced refill (one atomic on the
-    // global head + one unit per lane), so the global-load latency is paid once per 64
-    // fetches instead of on every fetch.
-    bool need = !done && !has;
-    uint64_t nm = __ballot(need);
-    while (nm) {
-      if (ring_next >= ring_cnt) {
-        if (ring_dead) break;
-        uint32_t base = 0;
-        if (lane == 0) base = static_end + atomicAdd(&cc[C_HEAD], (uint32_t)WAVE);
-        base = __shfl(base, 0);
-        if (base >= n_in) {
-          ring_dead = true;
-          break;
-        }
-        refill(base);
-      }
-      const uint32_t avail = ring_cnt - ring_next;
-      const uint32_t r = rank_in(nm);
-      if (need && r < avail) {
-        const uint32_t slot = ring_next + r;
-        uint32_t UK[MW];
-#pragma unroll
-        for (int w = 0; w < MW; ++w) {
-          T[w] = UR_(UL::T_ + w, slot);
-          D[w] = UR_(UL::D_ + w, slot);
-          UK[w] = UR_(UL::K_ + w, slot);
-        }
-        const uint32_t ud = UR_(UL::DEPTH, slot);
-        dlen = UR_(UL::DLEN, slot);
-        for (uint32_t i = 0; i < (dlen + 3) / 4; ++i) DOW_(i) = UR_(UL::ORD + i, slot);
-        ++tot_fetched;
-        seg_idx = ring_src + slot;
-        seg_open = true;
-        seg_count = seg_evals = seg_minq = seg_zfb = 0;
-#pragma unroll
-        for (int w = 0; w < MW; ++w) seg_K[w] = K[w] = UK[w];
-        seg_depth = depth = ud;
-        nst = 0;
-        sbase = 0;
-        need = false;
-        if (pruned(UK, ud)) close_segment();  // zero record
-        else has = true;
-      }
-      ring_next += min((uint32_t)__popcll(nm), avail);
-      nm = __ballot(need);
-    }
-    if (ring_dead && need) done = true;
-    if (!__any(has)) break;
+    QI_STAMP(0);  // pop / install
+    // lanes with nothing left: done (a claimed unit past the budget is spilled below)
+    if (!has && !tvalid && nst == 0 && !fpend && (pool_dead || steps >= limit)) done = true;
 
     // Every 32 iterations poll the global head and the device-side best key (one
     // blocking global load pair, kept off the per-iteration path).  Once no unit is left
-    // to fetch anywhere, every lane gets a short grace period and then spills: the next
+    // to claim anywhere, every lane gets a short grace period and then spills: the next
     // launch spreads the remaining subtrees over all lanes instead of letting a few lanes
     // grind through deep subtrees while the rest idle.
-    if ((iter++ & 31u) == 0u || (ring_dead && !dry)) {
+    if ((iter++ & 31u) == 0u) {
       uint32_t h = 0;
       uint64_t b = ~0ull;
       if (lane == 0) {
         h = static_end + __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      h = __shfl(h, 0);
-      best64 = __shfl(b, 0);
-      if (!dry && (ring_dead || h >= n_in)) {
+      h = lane0(h);
+      best64 = lane0(b);
+      if (!dry && h >= n_in) {
         dry = true;
         limit = min(limit, steps + a.grace);
       }
     }
 
-    QI_STAMP(1);  // fetch + polls
-    // ---- (3) budget exhausted: spill current node + stack to the next frontier --------
+    QI_STAMP(1);  // claims + polls
+    // ---- (3) budget exhausted: spill current node, top, stack and claimed unit ---------
     {
-      const bool spill = has && (steps >= limit || evictions >= a.evict_max);
+      const bool spill = (has && (steps >= limit || evictions >= a.evict_max)) ||
+                         (!has && fpend && steps >= limit);
       if (__any(spill)) {
         uint32_t total = 0;
-        const uint32_t n = spill ? 1u + nst : 0u;
-        uint32_t slot = reserve(n, &cc[C_OUT], total);
+        const uint32_t n = spill ? (has ? 1u : 0u) + (tvalid ? 1u : 0u) + nst + (fpend ? 1u : 0u) : 0u;
+        uint32_t slot = reserve<RB>(n, &cc[C_OUT], total);
         if (spill) {
-          write_unit(slot++, T, D, K, depth, dlen, -1);
-          for (uint32_t i = nst; i > 0; --i) write_entry(slot++, (sbase + i - 1) & (SMAX - 1));
+          if (has) write_unit(slot++, T, D, K, depth, dlen, -1);
+          if (tvalid) write_entry(slot++, tT, tD, tpk);
+          for (uint32_t i = nst; i > 0; --i) write_lds_entry(slot++, spos(i - 1));
+          if (fpend) write_claimed(slot++);
           nst = 0;
+          tvalid = false;
+          fpend = false;
+          if (seg_open) close_segment();
           has = false;
           done = true;
-          close_segment();
         }
       }
     }
+    if (!__any(!done)) break;
 
     QI_STAMP(2);  // spill
     // ---- (4) one search node per active lane (cpp:258-345) ---------------------------
@@ -686,6 +758,18 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = active2 ? (T[w] | D[w]) : 0u;
     const bool qne = EV::template gfp<0>(f, X, 0u, rounds);  // cpp:301
+#ifdef QI_ABL_GFP
+    {  // ablation: repeat both fixpoints on the same inputs (marginal cost measurement)
+      uint32_t Z[MW];
+#pragma unroll
+      for (int w = 0; w < MW; ++w) Z[w] = (active ? D[w] : 0u) ^ a.diag;
+      const bool r1 = EV::template gfp<0>(f, Z, 0u, rounds);
+#pragma unroll
+      for (int w = 0; w < MW; ++w) Z[w] = (active2 ? (T[w] | D[w]) : 0u) ^ a.diag;
+      const bool r2 = EV::template gfp<0>(f, Z, 0u, rounds);
+      if ((r1 ^ r2) && a.diag == 0x5EEDu) atomicOr(&a.glob[1], 64u);
+    }
+#endif
     QI_STAMP(3);  // the two fixpoints
     bool push = false;
     uint32_t pb = 0;
@@ -701,36 +785,57 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         has = false;
       } else {
         pb = EV::best(f, X, D, seg_zfb);  // cpp:317
+#ifdef QI_ABL_BEST
+        {
+          uint32_t Z[MW], zz = 0;
+#pragma unroll
+          for (int w = 0; w < MW; ++w) Z[w] = X[w] ^ a.diag;
+          if (EV::best(f, Z, D, zz) != pb && a.diag == 0x5EEDu) atomicOr(&a.glob[1], 64u);
+        }
+#endif
 #pragma unroll
         for (int w = 0; w < MW; ++w) X[w] &= ~D[w];
         X[pb >> 5] &= ~(1u << (pb & 31u));  // toRemove' = Q \ D \ {b} (cpp:330-334)
         push = true;
       }
     }
-    // push the inclusion branch (cpp:343-345); a full stack evicts its shallowest entry
-    // into the next frontier (wave-aggregated slot reservation, convergent).
+    // push the inclusion branch (cpp:343-345): the old top goes to LDS (a full stack
+    // first evicts its shallowest entry into the next frontier; wave-aggregated slot
+    // reservation, convergent), the new entry becomes the top.  Then continue with the
+    // exclusion branch (cpp:336): same D, T = T', key bit 0.
     {
-      const bool evict = push && nst == (uint32_t)SMAX;
+      const bool evict = push && tvalid && nst == (uint32_t)SMAX;
       if (__any(evict)) {
         uint32_t total = 0;
-        const uint32_t slot = reserve(evict ? 1u : 0u, &cc[C_OUT], total);
+        const uint32_t slot = reserve<1>(evict ? 1u : 0u, &cc[C_OUT], total);
         if (evict) {
-          write_entry(slot, sbase & (SMAX - 1));
-          sbase = (sbase + 1) & (SMAX - 1);
+          write_lds_entry(slot, spos(0));
+          sbase_ = spos(1);
           --nst;
           ++evictions;
         }
       }
       if (push) {
-        const uint32_t pos = (sbase + nst) & (SMAX - 1);
+        if (tvalid) {
+          const uint32_t pos = spos(nst);
+#pragma unroll
+          for (int w = 0; w < MW; ++w) {
+            ST_(pos, w) = tT[w];
+            ST_(pos, MW + w) = tD[w];
+          }
+          ST_(pos, 2 * MW) = tpk;
+          ++nst;
+        }
 #pragma unroll
         for (int w = 0; w < MW; ++w) {
-          ST_(pos, w) = X[w];
+          tT[w] = X[w];
+          tD[w] = D[w];
           T[w] = X[w];
         }
-        ST_(pos, MW) = pb | (depth << 8) | (dlen << 17);
-        ++nst;
-        ++depth;  // continue with the exclusion branch (cpp:336): key bit stays 0
+        tD[pb >> 5] |= 1u << (pb & 31u);
+        tpk = pb | (depth << 8) | (dlen << 17);
+        tvalid = true;
+        ++depth;
       }
     }
 
@@ -741,8 +846,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // Done per lane they would serialise the wave (the first removable vertex sits at a
     // ~uniform position of the D order), so they are spread over the wave in fixed slots
     // of S = a.coop_slot lanes per pending lane: lane l serves owner (l / S) of the
-    // current pass, job k = l % S (+ chunk offset when |D|+1 > S).  The owner's D arrives
-    // by __shfl, results by one LDS ds_or per successful job; one barrier per pass.
+    // current pass, job k = l % S (+ chunk offset when |D|+1 > S).  The owner's D, lane
+    // and |D| arrive through an LDS slot, results by one LDS ds_or per successful job.
     const uint64_t pm = __ballot(pending);
     if (pm) {
       ++coop_phases;
@@ -750,23 +855,24 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       const uint32_t r = rank_in(pm);
       const uint32_t S = a.coop_slot, lgS = a.coop_slot_log2;
       const uint32_t P = (uint32_t)WAVE >> lgS;  // owners per pass
-      if (pending) {
+      if (pending) {  // owner slot r: results zeroed, D / lane / |D| published
 #pragma unroll
         for (int w = 0; w < MW; ++w) {
           co_NE[w * WAVE + r] = 0u;
           co_VIS[w * WAVE + r] = 0u;
+          co_D[w * WAVE + r] = D[w];
         }
+        co_OWN[r] = lane | (dlen << 8);
       }
       __syncthreads();
       for (uint32_t q0 = 0; q0 < npend; q0 += P) {
         const uint32_t oi = q0 + (lane >> lgS);
-        uint64_t mm = pm;
-        for (uint32_t c = 0; c < oi && mm; ++c) mm &= mm - 1ull;  // oi-th pending lane
-        const uint32_t ol = mm ? (uint32_t)__builtin_ctzll(mm) : 0u;
+        const uint32_t oc = min(oi, (uint32_t)WAVE - 1u);  // slots >= npend: stale, masked by `act`
+        const uint32_t own = co_OWN[oc];
+        const uint32_t ol = own & 63u, dl = own >> 8;
         uint32_t Dr[MW];
 #pragma unroll
-        for (int w = 0; w < MW; ++w) Dr[w] = __shfl(D[w], (int)ol);
-        const uint32_t dl = __shfl(dlen, (int)ol);
+        for (int w = 0; w < MW; ++w) Dr[w] = co_D[w * WAVE + oc];
         for (uint32_t c0 = 0; c0 <= a.half_m; c0 += S) {  // jobs 0..|D| (|D| <= half_m)
           const uint32_t k = c0 + (lane & (S - 1u));
           const bool act = oi < npend && k <= dl;
@@ -783,6 +889,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             else Y[w] = Dr[w];
           }
           if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
+#ifdef QI_ABL_COOP
+          {
+            uint32_t Z[MW];
+#pragma unroll
+            for (int w = 0; w < MW; ++w) Z[w] = Y[w] ^ a.diag;
+            if (EV::template gfp<2>(f, Z, vis ? 1u : 0u, rounds) && a.diag == 0x5EEDu) atomicOr(&a.glob[1], 64u);
+          }
+#endif
           const bool ne = EV::template gfp<2>(f, Y, vis ? 1u : 0u, rounds);
           if (act && !vis && ne) atomicOr(&co_NE[(k >> 5) * WAVE + oi], 1u << (k & 31u));
           if (vis) {
@@ -824,6 +938,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             }
             atomicMin(a.best64, (unsigned long long)best_pack<MW>(K, depth));
             nst = 0;  // everything left in this unit follows the witness in preorder
+            tvalid = false;
           }
         } else {  // not minimal: isMinimal stops at the first removable vertex in D order
           uint32_t pos = 0;
@@ -835,28 +950,65 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
       __syncthreads();
     }
+    flush_record();
     QI_STAMP(5);  // quorum-leaf phase
-  }
-
-  // units claimed by this wave's ring but never fetched: carry them over unchanged
-  {
-    const uint32_t ring_pos = ring_src + ring_next;
-    const uint32_t left = (ring_next < ring_cnt) ? ring_cnt - ring_next : 0u;
-    if (left) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&cc[C_OUT], left);
-      base = __shfl(base, 0);
-      for (uint32_t i = lane; i < left; i += WAVE) {
-        const uint32_t src = ring_pos + i, dst = base + i;
-        uint32_t* r = records + (size_t)src * RL::WORDS;
-        for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
-        if (dst < a.out_cap) {
-          const uint4* s4 = (const uint4*)(a.units_in + (size_t)src * UW);
-          uint4* d4 = (uint4*)(a.units_out + (size_t)dst * UW);
-          for (int q = 0; q < UW / 4; ++q) d4[q] = s4[q];
-        } else {
-          atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
+    ++fage;
+    // ---- (6) claim the next units for the lanes that will need one in the next iteration
+    // (no node, no stacked entry left); the loads are in flight until the install.
+    // Indices come from a wave-uniform pool of 64 claimed with one atomic (a returning
+    // atomic per iteration would cost a memory round trip every iteration).
+    {
+      bool want = !done && !has && !fpend && !tvalid && nst == 0 && steps < limit;
+      uint64_t wm = __ballot(want);
+      while (wm) {
+        if (pool_next >= pool_end) {
+          if (pool_dead) break;
+          uint32_t base = 0;
+          if (lane == 0) base = static_end + atomicAdd(&cc[C_HEAD], (uint32_t)WAVE);
+          base = lane0(base);
+          if (base >= n_in) {
+            pool_dead = true;
+            break;
+          }
+          pool_next = base;
+          pool_end = min(base + (uint32_t)WAVE, n_in);
         }
+        const uint32_t avail = pool_end - pool_next;
+        const uint32_t r = rank_in(wm);
+        if (want && r < avail) {
+          fidx = pool_next + r;
+          fpend = true;
+          fage = 0;
+          want = false;
+          load_unit(fidx);
+        }
+        pool_next += min((uint32_t)__popcll(wm), avail);
+        wm = __ballot(want);
+      }
+      if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
+        dry = true;
+        limit = min(limit, steps + a.grace);
+      }
+    }
+  }
+  flush_record();
+
+  // indices of this wave's pool that no lane took: carry the units over unchanged
+  if (pool_next < pool_end) {
+    const uint32_t left = pool_end - pool_next;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&cc[C_OUT], left);
+    base = lane0(base);
+    for (uint32_t i = lane; i < left; i += WAVE) {
+      const uint32_t src = pool_next + i, dst = base + i;
+      uint32_t* r = records + (size_t)src * RL::WORDS;
+      for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
+      if (dst < a.out_cap) {
+        const uint4* s4 = (const uint4*)(a.units_in + (size_t)src * UW);
+        uint4* d4 = (uint4*)(a.units_out + (size_t)dst * UW);
+        for (int q = 0; q < UW / 4; ++q) d4[q] = s4[q];
+      } else {
+        atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
       }
     }
   }
@@ -895,15 +1047,15 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   {
     uint32_t old = 0;
     if (lane == 0) old = atomicAdd(&cc[C_DONE], 1u);
-    old = __shfl(old, 0);
+    old = lane0(old);
     if (old == nb_used - 1u) {
       uint32_t hd = 0, out = 0;
       if (lane == 0) {
         hd = atomicAdd(&cc[C_HEAD], 0u);
         out = atomicAdd(&cc[C_OUT], 0u);
       }
-      hd = __shfl(hd, 0);
-      out = __shfl(out, 0);
+      hd = lane0(hd);
+      out = lane0(out);
       const uint32_t head = (uint32_t)min((uint64_t)static_end + hd, (uint64_t)n_in);
       const uint32_t left = n_in - head;
       for (uint32_t i = lane; i < left; i += WAVE) {
@@ -931,7 +1083,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   }
 #undef ST_
 #undef DOW_
-#undef UR_
 }
 
 }  // namespace dev
