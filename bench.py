@@ -72,6 +72,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=["two_tier", "planted"], default="two_tier",
+                    help="two_tier: BASELINE configs[3] (intersecting, full search); planted: configs[4] "
+                         "(disjoint quorums planted late in preorder, early termination)")
     ap.add_argument("--k-top", type=int, default=10)
     ap.add_argument("--validators", type=int, default=256)
     ap.add_argument("--cpu-sample-nodes", type=int, default=4_000_000)
@@ -116,7 +119,8 @@ def main():
             comm_dev = torch.device("cpu")
     batch = args.batch or (64 if world == 1 else 8)
 
-    text = fbas_gen.two_tier(args.k_top, args.validators)
+    gen = fbas_gen.two_tier if args.workload == "two_tier" else fbas_gen.planted
+    text = gen(args.k_top, args.validators)
 
     # ---- time-to-verdict from JSON text (host parse + flatten + upload + solve), N=1 path
     t0 = time.perf_counter()
@@ -176,7 +180,8 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("k_top") == args.k_top and tj.get("validators") == args.validators:
+            if (tj.get("k_top") == args.k_top and tj.get("validators") == args.validators
+                    and tj.get("workload", "two_tier") == args.workload):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -200,7 +205,9 @@ def main():
         "dtype": "u32",
         "data": "synthetic (deterministic G2 generator, no random values)",
         "config": {
-            "workload": f"two_tier(k_top={args.k_top}, n={args.validators}) full search, no early exit",
+            "workload": (f"two_tier(k_top={args.k_top}, n={args.validators}) full search, no early exit"
+                         if args.workload == "two_tier" else
+                         f"planted(k_top={args.k_top}, n={args.validators}) disjoint quorums, early termination"),
             "validators": args.validators,
             "searched_scc": shape["m"],
             "search_nodes_per_step": res.nodes,

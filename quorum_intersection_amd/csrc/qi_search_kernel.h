@@ -478,6 +478,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #ifdef QI_STAMPS
   uint64_t stamp_sum[6] = {0, 0, 0, 0, 0, 0};
   uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
+  const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   uint64_t best64 = ~0ull;
 
@@ -605,6 +606,44 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     uint32_t* u = a.units_out + (size_t)slot * UW;
 #pragma unroll
     for (int q = 0; q < UW; ++q) u[q] = unit_word(q);
+  };
+
+  // claim the next units for the lanes that will need one in the next iteration (no node,
+  // no stacked entry left); the loads are in flight until the install.  Indices come
+  // from a wave-uniform pool of 64 claimed with one atomic (a returning atomic per
+  // iteration would cost a memory round trip every iteration).  Convergent.
+  auto claim = [&]() {
+    bool want = !done && !has && !fpend && !tvalid && nst == 0 && steps < limit;
+    uint64_t wm = __ballot(want);
+    while (wm) {
+      if (pool_next >= pool_end) {
+        if (pool_dead) break;
+        uint32_t base = 0;
+        if (lane == 0) base = static_end + atomicAdd(&cc[C_HEAD], (uint32_t)WAVE);
+        base = lane0(base);
+        if (base >= n_in) {
+          pool_dead = true;
+          break;
+        }
+        pool_next = base;
+        pool_end = min(base + (uint32_t)WAVE, n_in);
+      }
+      const uint32_t avail = pool_end - pool_next;
+      const uint32_t r = rank_in(wm);
+      if (want && r < avail) {
+        fidx = pool_next + r;
+        fpend = true;
+        fage = 0;
+        want = false;
+        load_unit(fidx);
+      }
+      pool_next += min((uint32_t)__popcll(wm), avail);
+      wm = __ballot(want);
+    }
+    if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
+      dry = true;
+      limit = min(limit, steps + a.grace);
+    }
   };
 
   for (;;) {
@@ -839,6 +878,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
+    // records of segments closed so far, then the unit loads of lanes that became free:
+    // both in flight during the cooperative phase below (the install waits on vmcnt,
+    // which counts stores and loads in issue order)
+    flush_record();
+    claim();
     QI_STAMP(4);  // findBestNode + push
     // ---- (5) quorum leaves: isMinimalQuorum + visitor, wave-cooperative --------------
     // Every pending lane (GFP(D) != ∅, cpp:281) needs |D| single-removal fixpoints
@@ -950,46 +994,12 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
       __syncthreads();
     }
-    flush_record();
     QI_STAMP(5);  // quorum-leaf phase
-    ++fage;
-    // ---- (6) claim the next units for the lanes that will need one in the next iteration
-    // (no node, no stacked entry left); the loads are in flight until the install.
-    // Indices come from a wave-uniform pool of 64 claimed with one atomic (a returning
-    // atomic per iteration would cost a memory round trip every iteration).
-    {
-      bool want = !done && !has && !fpend && !tvalid && nst == 0 && steps < limit;
-      uint64_t wm = __ballot(want);
-      while (wm) {
-        if (pool_next >= pool_end) {
-          if (pool_dead) break;
-          uint32_t base = 0;
-          if (lane == 0) base = static_end + atomicAdd(&cc[C_HEAD], (uint32_t)WAVE);
-          base = lane0(base);
-          if (base >= n_in) {
-            pool_dead = true;
-            break;
-          }
-          pool_next = base;
-          pool_end = min(base + (uint32_t)WAVE, n_in);
-        }
-        const uint32_t avail = pool_end - pool_next;
-        const uint32_t r = rank_in(wm);
-        if (want && r < avail) {
-          fidx = pool_next + r;
-          fpend = true;
-          fage = 0;
-          want = false;
-          load_unit(fidx);
-        }
-        pool_next += min((uint32_t)__popcll(wm), avail);
-        wm = __ballot(want);
-      }
-      if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
-        dry = true;
-        limit = min(limit, steps + a.grace);
-      }
+    if (pm) {  // lanes freed by the cooperative phase
+      flush_record();
+      claim();
     }
+    ++fage;
   }
   flush_record();
 
@@ -1037,6 +1047,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     atomicAdd(&tt[7], (unsigned long long)coop_phases);
 #ifdef QI_STAMPS
     for (int q = 0; q < 6; ++q) atomicAdd(&tt[8 + q], (unsigned long long)stamp_sum[q]);
+    atomicAdd(&tt[14], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - wave_t0));  // 100 MHz ticks
+    atomicAdd(&tt[15], 1ull);                                                           // waves
 #endif
   }
 

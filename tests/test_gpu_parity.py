@@ -227,7 +227,7 @@ def _two_way_search(text, hand_every=1, move_frac=0.5):
     L = _capi.lib()
     fa, fb = qa.FBAS(text), qa.FBAS(text)
     sa, sb = ctypes.c_void_p(), ctypes.c_void_p()
-    opts = _capi.SearchOpts(2, 8, 2, 2)
+    opts = _capi.SearchOpts(2, 8, 2, 2, 1)  # one launch per step: a hand-off after every launch
     _capi.check(L.qi_search_create(fa.handle, ctypes.byref(opts), ctypes.byref(sa)))
     _capi.check(L.qi_search_create(fb.handle, ctypes.byref(opts), ctypes.byref(sb)))
     _capi.check(L.qi_search_clear(sb))
@@ -307,5 +307,95 @@ def test_two_way_handoff_random_witness(seed):
     if not r["searched"]:
         pytest.skip("no search")
     d = _two_way_search(text, hand_every=1, move_frac=0.7)
+    assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"],
+                                                                 r["evals"] - r["scc_evals"], r["minq"])
+
+
+# ---- frontier growth + strided deal-out (distributed_search's hand-out, on one GPU) -----
+def _dealt_search(text, world, target, batch):
+    """Engine 0 grows the frontier to `target` units (qi_search_grow), every engine imports
+    all of it and keeps units[r::world] (qi_search_keep_strided); then chains of `batch`
+    launches per engine with best-key exchange, and preorder-filtered reduction."""
+    import ctypes
+    import torch
+    from quorum_intersection_amd import _capi
+    L = _capi.lib()
+    fbs = [qa.FBAS(text) for _ in range(world)]
+    ss = [ctypes.c_void_p() for _ in range(world)]
+    opts = _capi.SearchOpts(2, 16, 4, 2, batch)
+    for f, s in zip(fbs, ss):
+        _capi.check(L.qi_search_create(f.handle, ctypes.byref(opts), ctypes.byref(s)))
+    ub = L.qi_search_unit_bytes(ss[0])
+    kw = L.qi_search_key_words(ss[0])
+    info = _capi.StepInfo()
+    _capi.check(L.qi_search_grow(ss[0], target, ctypes.byref(info)))
+    n = L.qi_search_frontier(ss[0])
+    for s in ss[1:]:
+        _capi.check(L.qi_search_clear(s))  # the root lives on engine 0 only
+    if n:
+        buf = torch.empty(n * ub, dtype=torch.uint8, device="cuda")
+        _capi.check(L.qi_search_export(ss[0], n, ctypes.c_void_p(buf.data_ptr())))
+        for r, s in enumerate(ss):
+            _capi.check(L.qi_search_import(s, n, ctypes.c_void_p(buf.data_ptr())))
+            _capi.check(L.qi_search_keep_strided(s, r, world))
+        assert sum(L.qi_search_frontier(s) for s in ss) == n
+
+    def local_best(s):
+        k = (ctypes.c_uint32 * kw)()
+        d = ctypes.c_uint32()
+        return (list(k), d.value) if L.qi_search_local_best(s, k, ctypes.byref(d)) == 1 else None
+
+    while sum(L.qi_search_frontier(s) for s in ss):
+        for s in ss:
+            if L.qi_search_frontier(s):
+                _capi.check(L.qi_search_step(s, None))
+        keys = [k for k in (local_best(s) for s in ss) if k]
+        if keys:
+            k, d = min(keys)
+            for s in ss:
+                _capi.check(L.qi_search_set_best(s, (ctypes.c_uint32 * kw)(*k), d))
+    keys = [(k, s) for k, s in ((local_best(s), s) for s in ss) if k]
+    best = min(keys, key=lambda x: x[0]) if keys else None
+    tot = [0, 0, 0]
+    for s in ss:
+        t = _capi.Totals()
+        if best:
+            _capi.check(L.qi_search_reduce(s, (ctypes.c_uint32 * kw)(*best[0][0]), best[0][1], ctypes.byref(t)))
+        else:
+            _capi.check(L.qi_search_reduce(s, None, 0, ctypes.byref(t)))
+        tot[0] += t.nodes
+        tot[1] += t.evals
+        tot[2] += t.minq
+    res = {"verdict": best is None, "nodes": tot[0], "evals": tot[1], "minq": tot[2]}
+    if best:
+        q1 = (ctypes.c_uint32 * fbs[0].n)()
+        q2 = (ctypes.c_uint32 * fbs[0].n)()
+        l1, l2 = ctypes.c_uint32(), ctypes.c_uint32()
+        _capi.check(L.qi_search_witness(best[1], q1, ctypes.byref(l1), q2, ctypes.byref(l2)))
+        res["q1"], res["q2"] = list(q1)[: l1.value], list(q2)[: l2.value]
+    for s in ss:
+        L.qi_search_destroy(s)
+    return res
+
+
+@pytest.mark.parametrize("world,target,batch", [(2, 40, 1), (3, 200, 4), (5, 1000, 64)])
+@pytest.mark.parametrize("name", ["tiered_5", "broken", "planted_5_96", "tiered_5_shuffled"])
+def test_grow_deal_strided_exact(name, world, target, batch):
+    text = _text_for(name)
+    r = GOLD[name]
+    d = _dealt_search(text, world, target, batch)
+    assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"],
+                                                                 r["evals"] - r["scc_evals"], r["minq"])
+    if not r["verdict"]:
+        assert d["q1"] == r["q1"] and d["q2"] == r["q2"]
+
+
+@pytest.mark.parametrize("seed", [3, 8, 13])
+def test_grow_deal_strided_random_witness(seed):
+    text = random_org_fbas(seed, n_orgs=6 + seed % 3)
+    r = Oracle().load(text).solve()
+    if not r["searched"]:
+        pytest.skip("no search")
+    d = _dealt_search(text, 3, 64, 2)
     assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"],
                                                                  r["evals"] - r["scc_evals"], r["minq"])

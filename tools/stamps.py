@@ -1,4 +1,9 @@
-"""Diagnostic: section breakdown of the search loop (jit=3 stamp build) on the bench workload."""
+"""Diagnostic: section breakdown of the search loop (jit=3 stamp build) on the bench workload.
+
+Besides the per-section s_memtime shares it reports wave lifetimes (s_memrealtime,
+100 MHz) against the launch durations (HIP events): waves that finish before the slowest
+wave of their launch leave their slot idle until the launch ends.
+"""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -14,7 +19,15 @@ loc = be.reduce(None)
 st = loc["stamps"][:6]
 tot = sum(st)
 names = ["pop/close", "fetch+poll", "spill", "fixpoints", "best+push", "coop"]
+waves = max(loc["stamps"][7], 1)
+life_s = loc["stamps"][6] * 1e-8  # summed wave lifetimes
+kernel_s = be.kernel_ms * 1e-3
+cus = torch.cuda.get_device_properties(0).multi_processor_count
 print(json.dumps({"nodes": loc["nodes"], "wave_iters": loc["wave_iters"], "coop_phases": loc["coop_phases"],
                   "cycles_per_wave_iter": tot / max(loc["wave_iters"], 1),
                   "share": {n: round(v / tot, 4) for n, v in zip(names, st)},
-                  "cycles_per_iter": {n: round(v / max(loc["wave_iters"], 1), 1) for n, v in zip(names, st)}}, indent=1))
+                  "cycles_per_iter": {n: round(v / max(loc["wave_iters"], 1), 1) for n, v in zip(names, st)},
+                  "waves": waves, "launches": be.launches, "kernel_ms": be.kernel_ms,
+                  "avg_wave_life_us": 1e6 * life_s / waves,
+                  "loop_clock_ghz": tot / max(life_s, 1e-12) / 1e9,
+                  "wave_slot_use_7_per_cu": life_s / (kernel_s * 7 * cus)}, indent=1))
