@@ -56,6 +56,11 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
   search_body<MW, TW, SMAX, TableEval<MW, TW>>(a);
 }
 
+// Fold a host-known best witness into the device-side one (1-word keys).
+__global__ void min_best_kernel(unsigned long long* best64, unsigned long long v) {
+  if (threadIdx.x == 0) atomicMin(best64, v);
+}
+
 // out[i] = in[offset + i * stride]: a rank's strided share of a broadcast frontier.
 template <int MW>
 __global__ void gather_units_kernel(const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt, uint32_t* out) {
@@ -398,6 +403,7 @@ class SearchDeviceImpl : public SearchDevice {
     keep(d_.grp_extra = dupload(pad_rows(f.grp_extra, ge), stream_));
     for (uint32_t w = 0; w < 8; ++w) scc_mask_[w] = 0;
     for (uint32_t v = 0; v < f.m; ++v) scc_mask_[v >> 5] |= 1u << (v & 31);
+    for (uint32_t w = 0; w < 8; ++w) d_.scc_mask[w] = scc_mask_[w];
 
     cus_ = (uint32_t)device_cu_count(device_);
     max_blocks_ = cfg_.max_blocks ? cfg_.max_blocks : cus_ * 8u;  // refined below once shm_ is known
@@ -544,10 +550,13 @@ class SearchDeviceImpl : public SearchDevice {
     }
     a.has_best = has_best_ ? 1u : 0u;
     a.best_depth = best_depth_;
-    for (int w = 0; w < 8; ++w) {
-      a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
-      a.scc_mask[w] = scc_mask_[w];
+    for (int w = 0; w < 8; ++w) a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
+    if (MW == 1 && has_best_ && best_dirty_) {  // 1-word keys: the device best is exact; fold the host's in
+      hipLaunchKernelGGL(dev::min_best_kernel, dim3(1), dim3(64), 0, stream_, best64_,
+                         ((unsigned long long)best_key_[0] << 32) | best_depth_);
+      HIP_CHECK(hipGetLastError());
     }
+    best_dirty_ = false;
     HIP_CHECK(hipEventRecord(ev_[0], stream_));
     auto enqueue = [&](uint32_t k) {
       a.units_in = units_[(cur_ + k) & 1];
@@ -689,6 +698,7 @@ class SearchDeviceImpl : public SearchDevice {
     best_key_.resize(MW, 0);
     best_depth_ = depth;
     has_best_ = true;
+    best_dirty_ = true;
   }
 
   bool best(Witness* w) const override {
@@ -859,6 +869,7 @@ class SearchDeviceImpl : public SearchDevice {
   bool has_best_ = false;
   std::vector<uint32_t> best_key_;
   uint32_t best_depth_ = 0;
+  bool best_dirty_ = false;
   bool has_local_best_ = false;
   Witness local_best_;
   double sum_ms_ = 0;

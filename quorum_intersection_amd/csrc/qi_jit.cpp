@@ -177,7 +177,16 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
     o << "\n      const bool better = (low != 0xFFFFFFFFu) && (deg > bestdeg || (deg == bestdeg && low < bestv));"
       << " bestdeg = better ? deg : bestdeg; bestv = better ? low : bestv; }\n";
   }
-  o << "    zero_fallback += (bestdeg == 0u) ? 1u : 0u;\n    return bestv;\n  }\n};\n";
+  o << "    zero_fallback += (bestdeg == 0u) ? 1u : 0u;\n    return bestv;\n  }\n";
+  // the SCC mask and qmin as literals (no kernel-argument words held in SGPRs)
+  o << "  static __device__ __forceinline__ uint32_t scc_word(const LocalDev&, int w) {\n    return ";
+  for (int w = 0; w < MW; ++w) {
+    uint32_t word = 0;
+    for (uint32_t v = (uint32_t)w * 32; v < f.m && v < (uint32_t)w * 32 + 32; ++v) word |= 1u << (v & 31);
+    o << (w + 1 < MW ? "w == " + std::to_string(w) + " ? " + hex(word) + " : " : hex(word));
+  }
+  o << ";\n  }\n";
+  o << "  static __device__ __forceinline__ uint32_t qmin0(const LocalDev&) { return " << f.qmin[0] << "u; }\n};\n";
   o << "}  // namespace dev\n}  // namespace qi\n\n";
   o << "extern \"C\" __global__ __launch_bounds__(64) void qi_search_spec(qi::dev::SearchArgs a) {\n"
     << "  qi::dev::search_body<" << MW << ", " << TW << ", " << SMAX << ", qi::dev::SpecEval>(a);\n}\n";

@@ -53,6 +53,7 @@ struct LocalDev {
   const uint32_t* grp_extra;      // [E][MW]
   uint32_t T, R, G, m;
   uint32_t qmin0, qmin1;       // LocalFlat::qmin: |X| below it => empty fixpoint
+  uint32_t scc_mask[8];        // the searched SCC (all m local vertices)
 };
 
 // Wave-uniform tables are read through the constant address space so the compiler emits
@@ -205,6 +206,8 @@ struct TableEval {
                                                   uint32_t& zero_fallback) {
     return dev::best_node<MW>(f, Q, D, zero_fallback);
   }
+  static __device__ __forceinline__ uint32_t scc_word(const LocalDev& f, int w) { return f.scc_mask[w]; }
+  static __device__ __forceinline__ uint32_t qmin0(const LocalDev& f) { return f.qmin0; }
 };
 
 // ------------------------------------------------------------------------------------
@@ -276,7 +279,6 @@ struct SearchArgs {
   uint32_t has_best;             // host-known best key (multiword) for pruning
   uint32_t best_depth;
   uint32_t best_key[8];
-  uint32_t scc_mask[8];
   uint32_t diag;                 // 0; opaque to the compiler (keeps QI_ABL_* repeats alive)
 };
 
@@ -545,7 +547,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 
   auto pruned = [&](const uint32_t (&KK)[MW], uint32_t d) -> bool {
     bool p = false;
-    if (a.has_best) p = after_key<MW>(KK, d, a.best_key, a.best_depth);
+    // MW == 1: best64 is exact and the host writes its best there (no kernel-argument key)
+    if (MW > 1 && a.has_best) p = after_key<MW>(KK, d, a.best_key, a.best_depth);
     p = p || (best_pack<MW>(KK, d) > best64);
     return p;
   };
@@ -612,6 +615,33 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // no stacked entry left); the loads are in flight until the install.  Indices come
   // from a wave-uniform pool of 64 claimed with one atomic (a returning atomic per
   // iteration would cost a memory round trip every iteration).  Convergent.
+  // D is a minimal quorum (cpp:283-285): credit cpp:184, |D| x cpp:192 and the visitor
+  // (cpp:368); VIS = GFP(scc \ D) with outside vertices available.  A non-empty VIS is a
+  // disjoint quorum: record the witness, the unit ends here (cpp:369-377).
+  auto minimal_quorum = [&](const uint32_t (&VIS)[MW], bool vis_any) {
+    seg_evals += 2u + dlen;
+    ++seg_minq;
+    if (vis_any) {
+      const uint32_t slot = atomicAdd(&a.glob[0], 1u);
+      if (slot < a.wit_cap) {
+        uint32_t* wv = a.wit + (size_t)slot * WL::WORDS;
+#pragma unroll
+        for (int w = 0; w < MW; ++w) {
+          wv[w] = K[w];
+          wv[MW + 2 + w] = VIS[w];
+        }
+        wv[MW] = depth;
+        wv[MW + 1] = dlen;
+        for (uint32_t i = 0; i < (dlen + 3) / 4; ++i) wv[2 * MW + 2 + i] = DOW_(i);
+      } else {
+        atomicOr(&a.glob[1], FLAG_WIT_OVERFLOW);
+      }
+      atomicMin(a.best64, (unsigned long long)best_pack<MW>(K, depth));
+      nst = 0;  // everything left in this unit follows the witness in preorder
+      tvalid = false;
+    }
+  };
+
   auto claim = [&]() {
     bool want = !done && !has && !fpend && !tvalid && nst == 0 && steps < limit;
     uint64_t wm = __ballot(want);
@@ -892,6 +922,26 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // of S = a.coop_slot lanes per pending lane: lane l serves owner (l / S) of the
     // current pass, job k = l % S (+ chunk offset when |D|+1 > S).  The owner's D, lane
     // and |D| arrive through an LDS slot, results by one LDS ds_or per successful job.
+    // Quorum leaves with |D| - 1 < qmin: no D \ {v} can hold a quorum (LocalFlat::qmin),
+    // so D is minimal without evaluating them (still credited, as the reference makes the
+    // calls); only the visitor's fixpoint remains, evaluated here per lane.
+    {
+      const bool fastp = pending && dlen < EV::qmin0(f) + 1u;
+      if (__any(fastp)) {
+        uint32_t Y[MW];
+        uint32_t vany = 0;
+#pragma unroll
+        for (int w = 0; w < MW; ++w) Y[w] = fastp ? (EV::scc_word(f, w) & ~D[w]) : 0u;
+        EV::template gfp<1>(f, Y, 1u, rounds);  // visitor: scc \ Q, outside available
+#pragma unroll
+        for (int w = 0; w < MW; ++w) vany |= Y[w];
+        if (fastp) {
+          has = false;
+          pending = false;
+          minimal_quorum(Y, vany != 0u);
+        }
+      }
+    }
     const uint64_t pm = __ballot(pending);
     if (pm) {
       ++coop_phases;
@@ -929,7 +979,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll
           for (int w = 0; w < MW; ++w) {
             if (!act) Y[w] = 0u;
-            else if (vis) Y[w] = a.scc_mask[w] & ~Dr[w];  // visitor: scc \ Q, outside available
+            else if (vis) Y[w] = EV::scc_word(f, w) & ~Dr[w];  // visitor: scc \ Q, outside available
             else Y[w] = Dr[w];
           }
           if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
@@ -963,27 +1013,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
         has = false;
         if (!ne_any) {  // minimal quorum (cpp:283-285)
-          seg_evals += 2u + dlen;  // cpp:184, |D| x cpp:192, visitor cpp:368
-          ++seg_minq;
-          if (vis_any) {  // disjoint quorum: witness, the unit ends here (cpp:369-377)
-            const uint32_t slot = atomicAdd(&a.glob[0], 1u);
-            if (slot < a.wit_cap) {
-              uint32_t* wv = a.wit + (size_t)slot * WL::WORDS;
-#pragma unroll
-              for (int w = 0; w < MW; ++w) {
-                wv[w] = K[w];
-                wv[MW + 2 + w] = VIS[w];
-              }
-              wv[MW] = depth;
-              wv[MW + 1] = dlen;
-              for (uint32_t i = 0; i < (dlen + 3) / 4; ++i) wv[2 * MW + 2 + i] = DOW_(i);
-            } else {
-              atomicOr(&a.glob[1], FLAG_WIT_OVERFLOW);
-            }
-            atomicMin(a.best64, (unsigned long long)best_pack<MW>(K, depth));
-            nst = 0;  // everything left in this unit follows the witness in preorder
-            tvalid = false;
-          }
+          minimal_quorum(VIS, vis_any != 0u);
         } else {  // not minimal: isMinimal stops at the first removable vertex in D order
           uint32_t pos = 0;
 #pragma unroll
