@@ -33,7 +33,7 @@ struct SearchConfig {
   uint32_t max_blocks = 0;       // 0 = CUs * 8
   uint32_t grow_budget = 4;      // per-lane node budget while the frontier is small (sweep: 4 < 8 < 16 < 48 ms)
   uint32_t run_budget = 4096;    // per-lane node budget once the frontier fills the GPU
-  uint32_t grace = 64;           // per-lane steps after the unit queue runs dry
+  uint32_t grace = 24;           // per-lane steps after the unit queue runs dry (sweep: 16-48 best, 64+ worse)
   uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output)
   uint32_t batch = 0;            // max chained launches per step() (0 = 64)
   uint32_t lookahead = 2;        // launches kept in flight beyond the one the host waits for
