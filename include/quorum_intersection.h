@@ -148,6 +148,9 @@ typedef struct {
   double kernel_ms;
   uint32_t specialized;  /* 1 if this step ran the run-time specialised kernel */
   uint32_t launches;     /* chained launches of this step that had input */
+  uint32_t dispatches;   /* launches enqueued, incl. the <= 2 empty look-ahead ones */
+  uint32_t pad;
+  double dispatch_ms;    /* HIP-event time of all enqueued launches (what rocprof averages) */
 } qi_step_info;
 
 typedef struct {

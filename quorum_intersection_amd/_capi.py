@@ -73,6 +73,9 @@ class StepInfo(ctypes.Structure):
         ("kernel_ms", c_double),
         ("specialized", c_uint32),
         ("launches", c_uint32),
+        ("dispatches", c_uint32),
+        ("pad", c_uint32),
+        ("dispatch_ms", c_double),
     ]
 
 

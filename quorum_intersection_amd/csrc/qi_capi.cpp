@@ -3,6 +3,7 @@
 // qi_device.h; there is no CPU fallback: without a GPU every device entry point
 // returns QI_ERR_DEVICE.
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -120,9 +121,20 @@ SearchOutcome run_search(qi_fbas* f, const qi::SearchConfig& cfg) {
   if (qi::device_count() <= f->device || f->device < 0)
     throw qi::Error(QI_ERR_DEVICE, "no HIP device for the search (the MI355X path has no CPU fallback)");
   const auto& scc = f->sccs.members.front();
+  const bool trace = std::getenv("QI_TRACE") != nullptr;  // diagnostics: host-side phase times
+  auto t0 = std::chrono::steady_clock::now();
   qi::LocalFlat lf = qi::flatten_local(f->g, scc);
+  auto t1 = std::chrono::steady_clock::now();
   auto sd = qi::make_search_device(f->device, lf, cfg);
-  while (sd->frontier_size()) sd->step(0);
+  auto t2 = std::chrono::steady_clock::now();
+  int steps = 0;
+  while (sd->frontier_size()) {
+    sd->step(0);
+    ++steps;
+  }
+  if (trace)
+    std::fprintf(stderr, "[qi] flatten %.3f ms, create %.3f ms, %d steps %.3f ms\n", ms_since(t0) - ms_since(t1),
+                 ms_since(t1) - ms_since(t2), steps, ms_since(t2));
   SearchOutcome o;
   o.nonmonotone = lf.nonmonotone;
   qi::Witness w;
@@ -360,6 +372,9 @@ static int search_step(qi_search* s, uint64_t until, qi_step_info* info) {
       info->kernel_ms = si.kernel_ms;
       info->specialized = si.specialized ? 1u : 0u;
       info->launches = si.launches;
+      info->dispatches = si.dispatches;
+      info->pad = 0;
+      info->dispatch_ms = si.dispatch_ms;
     }
     return QI_OK;
   });

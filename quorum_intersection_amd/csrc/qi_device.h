@@ -50,6 +50,8 @@ struct StepInfo {
   uint64_t frontier_in = 0, frontier_out = 0;
   uint64_t processed = 0;        // input units of the launches of this step
   uint32_t launches = 0;         // launches that had input (the rest of the batch was empty)
+  uint32_t dispatches = 0;       // launches enqueued (incl. the <= lookahead empty ones)
+  double dispatch_ms = 0;        // HIP-event time of all enqueued launches
   uint32_t budget = 0, blocks = 0;
   uint64_t new_witnesses = 0;
   double kernel_ms = 0;          // HIP-event time of the search kernel
@@ -97,6 +99,8 @@ class SearchDevice {
   virtual void drop_log() = 0;                      // forget processed segments
   virtual double sum_kernel_ms() const = 0;
   virtual uint64_t launches() const = 0;
+  virtual uint64_t dispatches() const = 0;
+  virtual double dispatch_ms() const = 0;
   virtual uint64_t specialized_launches() const = 0;
   virtual bool wait_jit() = 0;                      // finish a pending compile; true if loaded
 };

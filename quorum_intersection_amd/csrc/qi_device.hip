@@ -23,6 +23,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <cstdio>
+#include <chrono>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -245,6 +248,38 @@ int device_cu_count(int device) {
 
 namespace {
 
+// hipStreamCreate costs ~2 ms on this stack (measured, QI_TRACE): engines take their stream
+// from a per-device pool and return it, so a solve does not pay it twice.
+struct StreamPool {
+  std::mutex mu;
+  std::vector<std::pair<int, hipStream_t>> free;
+};
+StreamPool& stream_pool() {
+  static StreamPool* p = new StreamPool;  // leaked on purpose: streams outlive static teardown
+  return *p;
+}
+hipStream_t acquire_stream(int device) {
+  {
+    std::lock_guard<std::mutex> g(stream_pool().mu);
+    auto& fr = stream_pool().free;
+    for (size_t i = 0; i < fr.size(); ++i)
+      if (fr[i].first == device) {
+        hipStream_t s = fr[i].second;
+        fr.erase(fr.begin() + (long)i);
+        return s;
+      }
+  }
+  hipStream_t s = nullptr;
+  HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return s;
+}
+void release_stream(int device, hipStream_t s) {
+  if (!s) return;
+  (void)hipStreamSynchronize(s);
+  std::lock_guard<std::mutex> g(stream_pool().mu);
+  stream_pool().free.emplace_back(device, s);
+}
+
 template <typename T>
 T* dalloc(size_t count) {
   void* p = nullptr;
@@ -273,7 +308,7 @@ class GfpDeviceImpl : public GfpDevice {
  public:
   GfpDeviceImpl(int device, const GlobalFlat& g) : device_(device) {
     DeviceGuard dg(device_);
-    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    stream_ = acquire_stream(device_);
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
     d_.n = g.n;
@@ -300,7 +335,7 @@ class GfpDeviceImpl : public GfpDevice {
     (void)hipFree(io_);
     (void)hipEventDestroy(e0_);
     (void)hipEventDestroy(e1_);
-    (void)hipStreamDestroy(stream_);
+    release_stream(device_, stream_);
   }
   void run(const uint64_t* nodes, const uint64_t* avail, uint32_t count, uint64_t* out) override {
     if (count == 0) return;
@@ -353,14 +388,24 @@ class SearchDeviceImpl : public SearchDevice {
   SearchDeviceImpl(int device, const LocalFlat& f, const SearchConfig& cfg)
       : device_(device), cfg_(cfg), m_(f.m), flat_(f) {
     DeviceGuard dg(device_);
+    trace_ = std::getenv("QI_TRACE") != nullptr;
+    auto tc0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+      if (!trace_) return;
+      const auto now = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "[qi]   ctor %-22s %.3f ms\n", what,
+                   std::chrono::duration<double, std::milli>(now - tc0).count());
+      tc0 = now;
+    };
     // tuning overrides for experiments (profiling only; defaults are the measured best)
     if (const char* e = std::getenv("QI_GRACE")) cfg_.grace = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
-    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    stream_ = acquire_stream(device_);
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
+    lap("stream/events");
     // pack one record per TN (TnRec layout), padded to the template's word counts
     using RC = dev::TnRec<MW, TW>;
     const uint32_t T = f.T;
@@ -401,6 +446,7 @@ class SearchDeviceImpl : public SearchDevice {
     keep(d_.grp_extra_off = dupload(f.grp_extra_off, stream_));
     const size_t ge = f.grp_extra_off.empty() ? 0 : f.grp_extra_off.back();
     keep(d_.grp_extra = dupload(pad_rows(f.grp_extra, ge), stream_));
+    lap("tables");
     for (uint32_t w = 0; w < 8; ++w) scc_mask_[w] = 0;
     for (uint32_t v = 0; v < f.m; ++v) scc_mask_[v >> 5] |= 1u << (v & 31);
     for (uint32_t w = 0; w < 8; ++w) d_.scc_mask[w] = scc_mask_[w];
@@ -414,7 +460,9 @@ class SearchDeviceImpl : public SearchDevice {
                             hipHostMallocMapped | hipHostMallocCoherent));
     HIP_CHECK(hipHostGetDevicePointer((void**)&hctr_dev_, (void*)hctr_, 0));
     glob_host_ = hctr_ + (size_t)kMaxBatch * dev::HC_WORDS;
+    lap("counters+pinned");
     for (auto& e : ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDefault));
+    lap("chain events");
     totals_ = dalloc<unsigned long long>(16 * dev::TOT_SHARDS);
     best64_ = dalloc<unsigned long long>(1);
     red_ = dalloc<unsigned long long>(4);
@@ -437,11 +485,14 @@ class SearchDeviceImpl : public SearchDevice {
                                                              shm_));
       if (nb > 0) max_blocks_ = cus_ * (uint32_t)nb;
     }
+    lap("occupancy");
     if ((cfg_.jit == 2 || cfg_.jit == 3) && jit_eligible(flat_)) {
       start_jit();
       if (!wait_jit()) throw Error(QI_ERR_UNSUPPORTED, "specialised kernel failed to build: " + jit_log_);
     }
+    lap("jit");
     reset_root();
+    lap("root");
   }
 
   ~SearchDeviceImpl() override {
@@ -462,7 +513,7 @@ class SearchDeviceImpl : public SearchDevice {
     (void)hipFree(wit_);
     (void)hipEventDestroy(e0_);
     (void)hipEventDestroy(e1_);
-    (void)hipStreamDestroy(stream_);
+    release_stream(device_, stream_);
   }
 
   uint32_t key_words() const override { return MW; }
@@ -595,6 +646,12 @@ class SearchDeviceImpl : public SearchDevice {
     double ms_sum = 0;
     uint64_t n_next = n_, log_next = lc.used;
     int cur_next = cur_;
+    for (uint32_t j = 0; j < enq; ++j) {
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, ev_[j], ev_[j + 1]));
+      si.dispatch_ms += ms;
+    }
+    si.dispatches = enq;
     for (; k < enq; ++k) {
       const volatile uint32_t* c = hc(k);
       if (!c[dev::HC_DONE]) throw Error(QI_ERR_DEVICE, "search launch did not publish its counters");
@@ -618,9 +675,12 @@ class SearchDeviceImpl : public SearchDevice {
     if (stopped) {
       const uint64_t need = first_need(n_);
       if (need > 0xFFFFFFF0ull) throw Error(QI_ERR_CAPACITY, "search frontier exceeds 2^32 units");
-      if (need > std::min(cap_[0], cap_[1])) {
-        ensure_cap(cur_, 2 * need, true);
-        ensure_cap(1 - cur_, 2 * need);
+      if (need > std::min(cap_[0], cap_[1])) {  // grow once to the full-grid bound (ramp stops
+        // cost a host round trip each)
+        const uint64_t full = std::min<uint64_t>(std::max<uint64_t>(4 * need, first_need((uint64_t)blocks * 64u * 16u)),
+                                                 0xFFFFFFF0ull);
+        ensure_cap(cur_, full, true);
+        ensure_cap(1 - cur_, full);
       }
       if (lc.cap - lc.used < n_) new_log_chunk(2 * n_);
       ++stops_;
@@ -635,6 +695,9 @@ class SearchDeviceImpl : public SearchDevice {
       for (uint32_t i = 0; i < nw; ++i) absorb_witness(&wv[(size_t)i * WL::WORDS]);
       si.new_witnesses = nw;
     }
+    if (trace_)
+      std::fprintf(stderr, "[qi]   step: %u launches enqueued, %u ran, frontier %llu, %s, kernel %.3f ms\n", enq, ran,
+                   (unsigned long long)n_, stopped ? "capacity stop" : "chain end", si.dispatch_ms);
     si.frontier_out = n_;
     si.budget = cfg_.run_budget;
     si.blocks = blocks;
@@ -644,6 +707,8 @@ class SearchDeviceImpl : public SearchDevice {
     si.specialized = spec;
     sum_ms_ += ms_sum;
     launches_ += ran;
+    dispatches_ += enq;
+    dispatch_ms_ += si.dispatch_ms;
     if (spec) spec_launches_ += ran;
     return si;
   }
@@ -771,11 +836,15 @@ class SearchDeviceImpl : public SearchDevice {
     has_local_best_ = false;
     sum_ms_ = 0;
     launches_ = 0;
+    dispatches_ = 0;
+    dispatch_ms_ = 0;
     spec_launches_ = 0;
   }
 
   double sum_kernel_ms() const override { return sum_ms_; }
   uint64_t launches() const override { return launches_; }
+  uint64_t dispatches() const override { return dispatches_; }
+  double dispatch_ms() const override { return dispatch_ms_; }
   uint64_t specialized_launches() const override { return spec_launches_; }
 
   bool wait_jit() override {
@@ -870,11 +939,14 @@ class SearchDeviceImpl : public SearchDevice {
   std::vector<uint32_t> best_key_;
   uint32_t best_depth_ = 0;
   bool best_dirty_ = false;
+  bool trace_ = false;
   bool has_local_best_ = false;
   Witness local_best_;
   double sum_ms_ = 0;
   uint64_t launches_ = 0;
   uint64_t spec_launches_ = 0;
+  uint64_t dispatches_ = 0;
+  double dispatch_ms_ = 0;
   // run-time specialisation (qi_jit.cpp)
   LocalFlat flat_;
   std::thread jit_thread_;

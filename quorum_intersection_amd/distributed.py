@@ -75,6 +75,8 @@ class DeviceSearch(SearchBackend):
         self.unit_bytes = int(self.L.qi_search_unit_bytes(h))
         self.kernel_ms = 0.0
         self.launches = 0
+        self.dispatches = 0
+        self.dispatch_ms = 0.0
         self.data_device = torch.device("cuda", fbas.device)  # where exported units live
 
     def close(self):
@@ -98,6 +100,8 @@ class DeviceSearch(SearchBackend):
         self._c.check(self.L.qi_search_restart(self.h))
         self.kernel_ms = 0.0
         self.launches = 0
+        self.dispatches = 0
+        self.dispatch_ms = 0.0
 
     def drop_log(self):
         # forget processed segments and bests but keep the current frontier
@@ -116,6 +120,8 @@ class DeviceSearch(SearchBackend):
         self._c.check(self.L.qi_search_step(self.h, ctypes.byref(info)))
         self.kernel_ms += info.kernel_ms
         self.launches += int(info.launches)
+        self.dispatches += int(info.dispatches)
+        self.dispatch_ms += info.dispatch_ms
         self.spec_launches = getattr(self, "spec_launches", 0) + int(info.specialized)
 
     def grow(self, target):
@@ -123,6 +129,8 @@ class DeviceSearch(SearchBackend):
         self._c.check(self.L.qi_search_grow(self.h, target, ctypes.byref(info)))
         self.kernel_ms += info.kernel_ms
         self.launches += int(info.launches)
+        self.dispatches += int(info.dispatches)
+        self.dispatch_ms += info.dispatch_ms
 
     def frontier(self) -> int:
         return int(self.L.qi_search_frontier(self.h))
