@@ -194,7 +194,9 @@ int qi_search_step(qi_search* s, qi_step_info* info);
 int qi_search_grow(qi_search* s, uint64_t target, qi_step_info* info);
 uint64_t qi_search_frontier(const qi_search* s);
 int qi_search_keep_slice(qi_search* s, uint64_t begin, uint64_t end);
-/* Keep units offset, offset + stride, ... (a rank's share of a broadcast frontier). */
+/* Keep a rank's share of a broadcast frontier: in round q (units q*stride .. q*stride +
+ * stride - 1) the unit at offset (offset - q) mod stride; the shares of offsets 0..stride-1
+ * partition the frontier. */
 int qi_search_keep_strided(qi_search* s, uint64_t offset, uint64_t stride);
 int qi_search_export(qi_search* s, uint64_t count, void* device_dst); /* pop `count` from the tail */
 int qi_search_import(qi_search* s, uint64_t count, const void* device_src);

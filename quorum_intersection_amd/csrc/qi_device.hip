@@ -64,12 +64,16 @@ __global__ void min_best_kernel(unsigned long long* best64, unsigned long long v
   if (threadIdx.x == 0) atomicMin(best64, v);
 }
 
-// out[i] = in[offset + i * stride]: a rank's strided share of a broadcast frontier.
+// A rank's share of a broadcast frontier, dealt in rounds of `stride` units with a rotating
+// offset: out[q] = in[q * stride + (offset - q) mod stride].  (A plain stride keeps any
+// period of the frontier order that divides it: spilled stacks alternate size classes, and
+// stride 8 once gave ranks 10 M vs 19 M nodes.)
 template <int MW>
 __global__ void gather_units_kernel(const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt, uint32_t* out) {
   using UL = UnitLayout<MW>;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint4* s4 = (const uint4*)(in + (offset + i * stride) * UL::WORDS);
+    const uint64_t src = i * stride + (offset + stride - i % stride) % stride;
+    const uint4* s4 = (const uint4*)(in + src * UL::WORDS);
     uint4* d4 = (uint4*)(out + i * UL::WORDS);
 #pragma unroll
     for (int q = 0; q < UL::WORDS / 4; ++q) d4[q] = s4[q];
@@ -400,6 +404,7 @@ class SearchDeviceImpl : public SearchDevice {
     // tuning overrides for experiments (profiling only; defaults are the measured best)
     if (const char* e = std::getenv("QI_GRACE")) cfg_.grace = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_STEAL")) cfg_.steal_max = (uint32_t)std::atoi(e);
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
     stream_ = acquire_stream(device_);
@@ -556,6 +561,10 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t blocks = max_blocks_;
     const uint32_t K = std::max(1u, std::min(cfg_.batch ? cfg_.batch : (uint32_t)kMaxBatch, (uint32_t)kMaxBatch));
     const uint32_t D = std::max(1u, cfg_.lookahead);
+    auto log_need = [&](uint64_t n) {  // the device's log check: n unit records + steals
+      const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
+      return n + nb * 64u * (cfg_.steal_max + 1u);
+    };
     auto first_need = [&](uint64_t n) {
       const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
       return n + nb * 64u * (smax + 3 + cfg_.evict_max);  // search_body's need_out
@@ -565,12 +574,12 @@ class SearchDeviceImpl : public SearchDevice {
       if (need > 0xFFFFFFF0ull) throw Error(QI_ERR_CAPACITY, "search frontier exceeds 2^32 units");
       ensure_cap(cur_, need, true);
       ensure_cap(1 - cur_, need);
-      if (log_.empty() || log_.back().cap - log_.back().used < n_) new_log_chunk(n_);
+      if (log_.empty() || log_.back().cap - log_.back().used < log_need(n_)) new_log_chunk(2 * log_need(n_));
     }
     LogChunk& lc = log_.back();
     uint32_t seed[dev::CTR_WORDS] = {0};
     seed[dev::C_OUT] = (uint32_t)n_;
-    seed[dev::C_LOGB] = (uint32_t)lc.used;
+    seed[dev::C_LOGN] = (uint32_t)lc.used;
     HIP_CHECK(hipMemcpyAsync(ctr_, seed, sizeof seed, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(ctr_ + dev::CTR_WORDS, 0, (size_t)K * dev::CTR_WORDS * 4, stream_));
     std::memset((void*)hctr_, 0, (size_t)K * dev::HC_WORDS * 4);
@@ -588,6 +597,7 @@ class SearchDeviceImpl : public SearchDevice {
     a.grow_budget = cfg_.grow_budget;
     a.run_budget = cfg_.run_budget;
     a.grace = cfg_.grace;
+    a.steal_max = cfg_.steal_max;
     a.evict_max = cfg_.evict_max;
     a.half_m = m_ / 2;
     {  // cooperative slot: smallest power of two covering |D| + 1 <= half_m + 1 jobs
@@ -661,7 +671,7 @@ class SearchDeviceImpl : public SearchDevice {
       }
       cur_next = (cur_ + k + 1) & 1;
       n_next = c[dev::HC_OUT];
-      log_next = (uint64_t)c[dev::HC_LOGB] + c[dev::HC_NIN];
+      log_next = c[dev::HC_LOGN];
       if (c[dev::HC_NIN] == 0) continue;
       ++ran;
       si.processed += c[dev::HC_NIN];
@@ -682,7 +692,7 @@ class SearchDeviceImpl : public SearchDevice {
         ensure_cap(cur_, full, true);
         ensure_cap(1 - cur_, full);
       }
-      if (lc.cap - lc.used < n_) new_log_chunk(2 * n_);
+      if (lc.cap - lc.used < log_need(n_)) new_log_chunk(2 * log_need(n_));
       ++stops_;
     }
     // collect new witnesses (the buffer restarts at 0 for the next step)
@@ -745,7 +755,11 @@ class SearchDeviceImpl : public SearchDevice {
   void keep_strided(uint64_t offset, uint64_t stride) override {
     DeviceGuard dg(device_);
     if (stride == 0) throw Error(QI_ERR_ARG, "keep_strided: stride 0");
-    const uint64_t cnt = offset < n_ ? (n_ - offset + stride - 1) / stride : 0;
+    // round q holds units [q*stride, (q+1)*stride); this rank's unit of round q is at
+    // q*stride + (offset - q) mod stride, present while that index is < n_
+    uint64_t cnt = n_ / stride;
+    if (cnt * stride + (offset + stride - cnt % stride) % stride < n_) ++cnt;
+    if (offset >= stride) cnt = 0;
     if (cnt) {
       ensure_cap(1 - cur_, cnt);
       const uint32_t nb = (uint32_t)std::min<uint64_t>((cnt + 255) / 256, 4096);
@@ -876,7 +890,7 @@ class SearchDeviceImpl : public SearchDevice {
 
   void new_log_chunk(uint64_t min_cap) {
     LogChunk c;
-    c.cap = std::max<uint64_t>(min_cap, 1u << 22);
+    c.cap = std::max<uint64_t>(min_cap, 1u << 23);
     c.cap = std::min<uint64_t>(c.cap, 0xFFFFFFF0ull);
     c.ptr = dalloc<uint32_t>(c.cap * RL::WORDS);
     c.used = 0;

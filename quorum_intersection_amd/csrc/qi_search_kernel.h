@@ -244,12 +244,14 @@ enum : int {
   C_OUT = 0,       // units written to units_out (spills + carried-over units)   [atomic]
   C_HEAD = 1,      // dynamic claims past the statically assigned range           [atomic]
   C_DONE = 2,      // used blocks that finished                                   [atomic]
+  C_XREC = 3,      // log records of stolen segments (after the n_in unit records) [atomic]
   C_NIN = 32,      // input units of this launch (the previous block's C_OUT)
   C_LOGB = 33,     // first segment-log record of this launch
   C_STOP = 34,     // 1: capacity would be exceeded; this launch (and the rest of the chain) did nothing
   C_STATIC = 35,   // end of the statically assigned range (64 units per used block)
+  C_LOGN = 36,     // log base of the next launch (written by this launch's last block)
   CTR_WORDS = 64,
-  HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_WORDS = 8
+  HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_WORDS = 8
 };
 constexpr int TOT_SHARDS = 64;  // running totals: [TOT_SHARDS][16] u64, shard = block % 64
 
@@ -272,6 +274,7 @@ struct SearchArgs {
   uint32_t grow_budget;          // per-lane node budget while the frontier is below half the lanes
   uint32_t run_budget;
   uint32_t grace;                // extra steps per lane once the unit queue is dry
+  uint32_t steal_max;            // stacked entries a lane may take from busy lanes per launch
   uint32_t evict_max;
   uint32_t half_m;
   uint32_t coop_slot;            // lanes per pending owner in the cooperative phase (pow2)
@@ -408,20 +411,23 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     return;
   }
   const uint32_t n_in = pc[C_OUT];
-  const uint32_t log_base = pc[C_LOGB] + pc[C_NIN];
+  const uint32_t log_base = pc[C_LOGN];
   const uint32_t nb_used = min((n_in + (uint32_t)WAVE - 1u) / (uint32_t)WAVE, gridDim.x);
   const uint32_t static_end = min(n_in, nb_used * (uint32_t)WAVE);
   {
     // per lane at most: current node + top of stack + SMAX entries + a prefetched unit
     // spilled once, plus evict_max evictions
     const uint64_t need_out = (uint64_t)n_in + (uint64_t)nb_used * WAVE * (uint64_t)(SMAX + 3 + a.evict_max);
-    const bool stop = need_out > (uint64_t)a.out_cap || (uint64_t)log_base + n_in > (uint64_t)a.log_cap;
+    const uint64_t need_log = (uint64_t)log_base + n_in + (uint64_t)nb_used * WAVE * (a.steal_max + 1u);
+    const bool stop = need_out > (uint64_t)a.out_cap || need_log > (uint64_t)a.log_cap;
     if (blockIdx.x == 0 && lane == 0) {
       cc[C_NIN] = n_in;
       cc[C_LOGB] = log_base;
       cc[C_STATIC] = static_end;
       cc[C_STOP] = stop ? 1u : 0u;
       if (stop || nb_used == 0) {  // nothing runs: publish now (else the last block does)
+        cc[C_LOGN] = log_base;
+        a.host_ctr[HC_LOGN] = log_base;
         a.host_ctr[HC_OUT] = 0u;
         a.host_ctr[HC_NIN] = n_in;
         a.host_ctr[HC_LOGB] = log_base;
@@ -456,7 +462,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     const uint32_t p = sbase_ + i;
     return p >= (uint32_t)SMAX ? p - (uint32_t)SMAX : p;
   };
-  uint32_t steps = 0, evictions = 0;
+  uint32_t steps = 0, evictions = 0, steals = 0;
+  uint32_t xpool_next = 0, xpool_end = 0;  // wave-uniform: claimed extra log record slots
   uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
   bool dry = false;         // wave-uniform: no unit left to claim (head >= n_in)
   uint32_t iter = 0;
@@ -750,9 +757,92 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
+    // ---- (1b) once this wave's pool is dry, idle lanes take the bottom (shallowest,
+    // largest) stacked entry of a busy lane of the wave.  That subtree is the last part of
+    // the donor's unit in preorder, so it becomes a segment of its own (log record after
+    // this launch's n_in unit records) and counts stay preorder-exact; the donor keeps
+    // the rest.  The k-th idle lane pairs with the k-th donor through an LDS slot.
+    if (pool_dead) {
+      const bool idle = !done && !has && !tvalid && nst == 0 && !fpend && steps < limit && steals < a.steal_max;
+      const uint64_t im = __ballot(idle);
+      if (im) {
+        const uint64_t gm = __ballot(nst > 0u);
+        const uint32_t np = min((uint32_t)__popcll(im), (uint32_t)__popcll(gm));
+        if (np) {
+          const uint32_t ri = rank_in(im), rg = rank_in(gm);
+          if (nst > 0u && rg < np) {  // donor: publish lane, entry position and key
+            co_OWN[rg] = lane | (spos(0) << 8);
+#pragma unroll
+            for (int w = 0; w < MW; ++w) co_D[w * WAVE + rg] = K[w];
+            sbase_ = spos(1);
+            --nst;
+          }
+          if (xpool_end - xpool_next < np) {  // extra record slots, 64 per atomic (the rest of
+            // an old pool is zero-filled: every slot of the log range must be written)
+            for (uint32_t i = xpool_next + lane; i < xpool_end; i += WAVE) {
+              uint32_t* r = records + (size_t)(n_in + i) * RL::WORDS;
+#pragma unroll
+              for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
+            }
+            uint32_t xb = 0;
+            if (lane == 0) xb = atomicAdd(&cc[C_XREC], (uint32_t)WAVE);
+            xpool_next = lane0(xb);
+            xpool_end = xpool_next + (uint32_t)WAVE;
+          }
+          const uint32_t xbase = xpool_next;
+          xpool_next += np;
+          if (idle && ri < np) {  // receiver: the entry becomes its unit
+            const uint32_t own = co_OWN[ri];
+            const uint32_t dl = own & 63u, pos = own >> 8;
+            const uint32_t* ent = st + (size_t)pos * SE * WAVE + dl;
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+              T[w] = ent[w * WAVE];
+              D[w] = ent[(MW + w) * WAVE];
+              K[w] = co_D[w * WAVE + ri];
+            }
+            const uint32_t pk = ent[2 * MW * WAVE];
+            const uint32_t b = pk & 255u, de = (pk >> 8) & 511u, dle = pk >> 17;
+            key_prefix_bit<MW>(K, de);
+            depth = de + 1;
+            dlen = dle + 1;
+            const uint32_t nw = (dle + 3) / 4;  // the donor's D order below the entry, then b
+            if constexpr (OW <= 8) {
+              uint32_t ow[OW];
+#pragma unroll
+              for (int i = 0; i < OW; ++i) ow[i] = ((uint32_t)i < nw) ? dow[i * WAVE + dl] : 0u;
+#pragma unroll
+              for (int i = 0; i < OW; ++i)
+                if ((uint32_t)i < nw) DOW_(i) = ow[i];
+            } else {
+              for (uint32_t i = 0; i < nw; ++i) DOW_(i) = dow[i * WAVE + dl];
+            }
+            set_ord(dle, b);
+            ++steals;
+            seg_idx = n_in + xbase + ri;
+            seg_open = true;
+            seg_count = seg_evals = seg_minq = seg_zfb = 0;
+#pragma unroll
+            for (int w = 0; w < MW; ++w) seg_K[w] = K[w];
+            seg_depth = depth;
+            nst = 0;
+            sbase_ = 0;
+            tvalid = false;
+            if (pruned(K, depth)) close_segment();
+            else has = true;
+          }
+        }
+      }
+    }
+
     QI_STAMP(0);  // pop / install
     // lanes with nothing left: done (a claimed unit past the budget is spilled below)
-    if (!has && !tvalid && nst == 0 && !fpend && (pool_dead || steps >= limit)) done = true;
+    {  // a lane with nothing left is done once it cannot get a unit or steal any more
+      const bool wave_busy = __any(has || tvalid || nst > 0u);
+      if (!has && !tvalid && nst == 0 && !fpend &&
+          (steps >= limit || (pool_dead && (!wave_busy || steals >= a.steal_max))))
+        done = true;
+    }
 
     // Every 32 iterations poll the global head and the device-side best key (one
     // blocking global load pair, kept off the per-iteration path).  Once no unit is left
@@ -1032,6 +1122,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     ++fage;
   }
   flush_record();
+  for (uint32_t i = xpool_next + lane; i < xpool_end; i += WAVE) {  // unused extra record slots
+    uint32_t* r = records + (size_t)(n_in + i) * RL::WORDS;
+#pragma unroll
+    for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
+  }
 
   // indices of this wave's pool that no lane took: carry the units over unchanged
   if (pool_next < pool_end) {
@@ -1112,9 +1207,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
         }
       }
+      uint32_t xr = 0;
+      if (lane == 0) xr = atomicAdd(&cc[C_XREC], 0u);
+      xr = lane0(xr);
       if (lane == 0) {
         out += left;
         if (left) atomicExch(&cc[C_OUT], out);
+        cc[C_LOGN] = log_base + n_in + xr;
+        a.host_ctr[HC_LOGN] = log_base + n_in + xr;
         a.host_ctr[HC_OUT] = out;
         a.host_ctr[HC_NIN] = n_in;
         a.host_ctr[HC_LOGB] = log_base;

@@ -6,8 +6,9 @@ by branch prefix:
   1. rank 0 grows the frontier from the root (cpp:393) with a short chain of device
      launches until it holds ``seed_units`` subtree units (branch prefixes);
   2. it broadcasts those units (one RCCL broadcast of packed unit bytes), and every rank
-     keeps the strided share ``units[rank::world]`` -- neighbouring prefixes have
-     correlated subtree sizes, so a strided deal balances better than contiguous slices;
+     keeps its dealt share (rounds of ``world`` units, offset rotating by one per round) --
+     neighbouring prefixes have correlated subtree sizes, so a deal balances better than
+     contiguous slices, and the rotation breaks periodic patterns in the frontier order;
   3. every rank runs chains of device launches on its own units; between chains the
      ranks exchange only frontier sizes + best-witness keys (one all_gather of a few
      int64s) and, when some rank would idle part of its GPU while another holds surplus,
@@ -300,7 +301,7 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
         n = torch.tensor([be.frontier() if rank == 0 else 0], dtype=torch.int64, device=device)
         dist.broadcast(n, 0, group=group)
         n = int(n.item())
-        # (2) ... hands it to every rank; each keeps the strided share units[rank::world]
+        # (2) ... hands it to every rank; each keeps its dealt share (rotating offset)
         if rank != 0:
             be.clear()
         if n:

@@ -99,8 +99,8 @@ class FakeSearch(SearchBackend):
     def keep_slice(self, b, e):
         self.units = self.units[b:e]
 
-    def keep_strided(self, offset, stride):
-        self.units = self.units[offset::stride]
+    def keep_strided(self, offset, stride):  # rotating deal, as qi_search_keep_strided
+        self.units = [u for i, u in enumerate(self.units) if (i // stride + i) % stride == offset]
 
     def grow(self, target):
         while self.units and len(self.units) < target:

@@ -399,3 +399,16 @@ def test_grow_deal_strided_random_witness(seed):
     d = _dealt_search(text, 3, 64, 2)
     assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"],
                                                                  r["evals"] - r["scc_evals"], r["minq"])
+
+
+# ---- intra-wave stealing (off by default; QI_STEAL = entries per lane per launch) ---------
+@pytest.mark.parametrize("name", ["tiered_5", "tiered_6", "broken", "planted_5_96", "tiered_5_shuffled"])
+def test_stealing_exact(name, monkeypatch):
+    monkeypatch.setenv("QI_STEAL", "16")
+    text = _text_for(name)
+    r = GOLD[name] if name in GOLD else Oracle().load(text).solve()
+    for jit in (1, 2):
+        d = qa.FBAS(text).solve_stats(jit=jit, grow_budget=2, run_budget=64)
+        assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"], r["evals"], r["minq"])
+        if not r["verdict"]:
+            assert d["q1"] == r["q1"] and d["q2"] == r["q2"]
