@@ -84,7 +84,7 @@ def main():
     ap.add_argument("--run-budget", type=int, default=0)
     ap.add_argument("--max-blocks", type=int, default=0)
     ap.add_argument("--batch", type=int, default=0,
-                    help="launches per chain between host synchronisations (0: 64 at N=1, 8 at N>1)")
+                    help="launches per chain between host synchronisations and rank exchanges (0 = 64)")
     ap.add_argument("--seed-units", type=int, default=0,
                     help="N>1: units rank 0 grows and deals out (0 = 2048 per rank)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -117,7 +117,7 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
             comm_dev = torch.device("cpu")
-    batch = args.batch or (64 if world == 1 else 8)
+    batch = args.batch or 64  # dealt shares are balanced to a few %: exchange only between full chains
 
     gen = fbas_gen.two_tier if args.workload == "two_tier" else fbas_gen.planted
     text = gen(args.k_top, args.validators)

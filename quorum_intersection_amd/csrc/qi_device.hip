@@ -560,7 +560,8 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t smax = spec ? (uint32_t)jit_smax_ : (uint32_t)SMAX;
     const uint32_t blocks = max_blocks_;
     const uint32_t K = std::max(1u, std::min(cfg_.batch ? cfg_.batch : (uint32_t)kMaxBatch, (uint32_t)kMaxBatch));
-    const uint32_t D = std::max(1u, cfg_.lookahead);
+    // growing to a target: no look-ahead, so the chain stops at the first launch past it
+    const uint32_t D = until ? 0u : std::max(1u, cfg_.lookahead);
     auto log_need = [&](uint64_t n) {  // the device's log check: n unit records + steals
       const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
       return n + nb * 64u * (cfg_.steal_max + 1u);
