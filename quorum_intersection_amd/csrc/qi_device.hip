@@ -405,6 +405,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_GRACE")) cfg_.grace = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_STEAL")) cfg_.steal_max = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
     stream_ = acquire_stream(device_);
@@ -599,6 +600,7 @@ class SearchDeviceImpl : public SearchDevice {
     a.run_budget = cfg_.run_budget;
     a.grace = cfg_.grace;
     a.steal_max = cfg_.steal_max;
+    a.run_at = cfg_.run_at;
     a.evict_max = cfg_.evict_max;
     a.half_m = m_ / 2;
     {  // cooperative slot: smallest power of two covering |D| + 1 <= half_m + 1 jobs

@@ -275,6 +275,7 @@ struct SearchArgs {
   uint32_t run_budget;
   uint32_t grace;                // extra steps per lane once the unit queue is dry
   uint32_t steal_max;            // stacked entries a lane may take from busy lanes per launch
+  uint32_t run_at;               // run budget once n_in >= run_at/8 of the resident lanes
   uint32_t evict_max;
   uint32_t half_m;
   uint32_t coop_slot;            // lanes per pending owner in the cooperative phase (pow2)
@@ -438,7 +439,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     if (stop || blockIdx.x >= nb_used) return;
   }
   uint32_t* const records = a.records + (size_t)log_base * RL::WORDS;
-  const uint32_t budget = (n_in >= gridDim.x * (uint32_t)WAVE / 2u) ? a.run_budget : a.grow_budget;
+  const uint32_t budget = ((uint64_t)n_in * 8u >= (uint64_t)gridDim.x * WAVE * a.run_at) ? a.run_budget : a.grow_budget;
 #define ST_(lvl, w) st[((lvl) * SE + (w)) * WAVE + lane]
 #define DOW_(w) dow[(w) * WAVE + lane]
   // byte i of this lane's D order (ds_write_b8 into the packed word)
