@@ -34,7 +34,8 @@ struct SearchConfig {
   uint32_t grow_budget = 2;      // per-lane node budget while the frontier is small (sweeps: 2 < 4 < 8 < 16 < 48 ms)
   uint32_t run_budget = 4096;    // per-lane node budget once the frontier fills the GPU
   uint32_t grace = 24;           // per-lane steps after the unit queue runs dry (sweep: 16-48 best, 64+ worse)
-  uint32_t evict_max = 8;        // per-lane stack evictions per launch (bounds the output; 8/32/64 measured equal)
+  uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output; 8 stalls deep
+                                 // multi-word searches, 8/32/64 equal on the bench)
   uint32_t run_at = 4;           // run budget once the frontier holds >= run_at/8 of the resident lanes
   uint32_t steal_max = 0;        // per-lane entries taken from busy lanes per launch (bounds the log);
                                  // 0 = off: measured 4.6 vs 4.0 ms per search with 16 (QI_STEAL)
