@@ -199,7 +199,8 @@ std::vector<char> jit_compile(const std::string& src, std::string* log) {
   }
   const std::string dir = cache_dir();
   char key[32];
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v1"));
+  const char* xf = std::getenv("QI_JIT_FLAGS");
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v1|" + (xf ? xf : "")));
   const std::string path = dir + "/" + key + ".co";
   {
     std::ifstream in(path, std::ios::binary);
@@ -213,8 +214,15 @@ std::vector<char> jit_compile(const std::string& src, std::string* log) {
     if (log) *log = "hiprtcCreateProgram failed";
     return {};
   }
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pragma-once-outside-header"};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+  std::vector<std::string> optv = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pragma-once-outside-header"};
+  if (const char* e = std::getenv("QI_JIT_FLAGS")) {  // diagnostics: extra compiler flags (space separated)
+    std::istringstream is(e);
+    std::string t;
+    while (is >> t) optv.push_back(t);
+  }
+  std::vector<const char*> opts;
+  for (auto& o : optv) opts.push_back(o.c_str());
+  const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   size_t n = 0;
   hiprtcGetProgramLogSize(prog, &n);
   std::string lg(n, '\0');
