@@ -72,11 +72,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=["two_tier", "planted"], default="two_tier",
-                    help="two_tier: BASELINE configs[3] (intersecting, full search); planted: configs[4] "
-                         "(disjoint quorums planted late in preorder, early termination)")
-    ap.add_argument("--k-top", type=int, default=10)
-    ap.add_argument("--validators", type=int, default=256)
+    ap.add_argument("--workload", choices=["two_tier", "planted_deep", "planted"], default="two_tier",
+                    help="two_tier: BASELINE configs[3] (intersecting, full search); planted_deep: configs[4] "
+                         "(512 validators, first witness 1.90M nodes into a 4.75M-node tree: early termination "
+                         "and rebalancing); planted: shallow planted pair (witness plumbing only)")
+    ap.add_argument("--k-top", type=int, default=None, help="tier organisations (default 10; planted_deep 8)")
+    ap.add_argument("--validators", type=int, default=None, help="default 256; planted_deep 512")
     ap.add_argument("--cpu-sample-nodes", type=int, default=4_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -92,6 +93,11 @@ def main():
     ap.add_argument("--jit", type=int, default=2,
                     help="0 auto, 1 table-interpreting kernel only, 2 run-time specialised kernel (default)")
     args = ap.parse_args()
+    deep = args.workload == "planted_deep"
+    if args.k_top is None:
+        args.k_top = 8 if deep else 10
+    if args.validators is None:
+        args.validators = 512 if deep else 256
 
     import torch
     import torch.distributed as dist
@@ -119,7 +125,7 @@ def main():
             comm_dev = torch.device("cpu")
     batch = args.batch or 64  # dealt shares are balanced to a few %: exchange only between full chains
 
-    gen = fbas_gen.two_tier if args.workload == "two_tier" else fbas_gen.planted
+    gen = {"two_tier": fbas_gen.two_tier, "planted": fbas_gen.planted, "planted_deep": fbas_gen.planted_deep}[args.workload]
     text = gen(args.k_top, args.validators)
 
     # ---- HIP runtime / device initialisation, reported apart from time-to-verdict (the
@@ -221,9 +227,12 @@ def main():
         "dtype": "u32",
         "data": "synthetic (deterministic G2 generator, no random values)",
         "config": {
-            "workload": (f"two_tier(k_top={args.k_top}, n={args.validators}) full search, no early exit"
-                         if args.workload == "two_tier" else
-                         f"planted(k_top={args.k_top}, n={args.validators}) disjoint quorums, early termination"),
+            "workload": {
+                "two_tier": f"two_tier(k_top={args.k_top}, n={args.validators}) full search, no early exit",
+                "planted_deep": f"planted_deep(k={args.k_top}, n={args.validators}) disjoint quorums deep in "
+                                f"preorder, early termination",
+                "planted": f"planted(k_top={args.k_top}, n={args.validators}) disjoint quorums, early termination",
+            }[args.workload],
             "validators": args.validators,
             "searched_scc": shape["m"],
             "search_nodes_per_step": res.nodes,

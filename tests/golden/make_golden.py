@@ -7,6 +7,7 @@ facts) is produced by the oracle under the deterministic "lowest index" tie-brea
 findBestNode (cpp:203-250) and pinned so later rounds cannot drift.
 
     python tests/golden/make_golden.py
+    python tests/golden/make_golden.py --big [name prefix ...]   # golden_big.json
 """
 import json
 import os
@@ -36,21 +37,35 @@ def instances():
         yield f"random_{s}", random_fbas(s)
 
 
-def big():
-    """Bench-size instances (minutes of single-threaded oracle time each)."""
-    o = Oracle()
-    out = {}
+def big_instances():
     for k in (9, 10):
-        r = o.load(fbas_gen.two_tier(k, 256)).solve()
-        out[f"two_tier_{k}_256"] = {"verdict": r["verdict"], "nodes": r["nodes"], "evals": r["evals"],
-                                    "minq": r["minq"], "nscc": r["nscc"], "oracle_seconds": round(r["seconds"], 2)}
-    with open(os.path.join(HERE, "golden_big.json"), "w") as f:
+        yield f"two_tier_{k}_256", fbas_gen.two_tier(k, 256)
+    # BASELINE configs[4]: the planted pair lies past 40% of the tree; "_intact" is the same
+    # FBAS without the pair (plant=False), whose full search sizes the tree
+    yield "planted_deep_8_512", fbas_gen.planted_deep(8, 512)
+    yield "planted_deep_8_512_intact", fbas_gen.planted_deep(8, 512, plant=False)
+
+
+def big(only):
+    """Bench-size instances (minutes of single-threaded oracle time each); `only` = name
+    prefixes to regenerate, the other entries are kept."""
+    path = os.path.join(HERE, "golden_big.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    o = Oracle()
+    for name, text in big_instances():
+        if only and not any(name.startswith(p) for p in only):
+            continue
+        r = o.load(text).solve()
+        out[name] = {k: r[k] for k in KEYS}
+        out[name]["oracle_seconds"] = round(r["seconds"], 2)
+        print(name, out[name]["nodes"], out[name]["oracle_seconds"], flush=True)
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
 
 
 def main():
     if "--big" in sys.argv:
-        return big()
+        return big(sys.argv[sys.argv.index("--big") + 1:])
     o = Oracle()
     out = {}
     for name, text in instances():

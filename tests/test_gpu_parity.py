@@ -52,13 +52,12 @@ def _text_for(name):
     return random_fbas(int(name.split("_")[1]))
 
 
-def _validate_witness(text, q1, q2):
+def _validate_witness(text, q1, q2, front=None):
     """Independent witness check with the oracle's slice predicate: Q1 ∩ Q2 = ∅, both in
     the main SCC, every v in Q2 has a slice inside Q2 (outside unavailable), every v in
     Q1 has a slice inside Q1 ∪ (V \\ scc) (outside available, cpp:354/368)."""
     g = Oracle().load(text)
-    r = g.solve()
-    scc = set(r["front"])
+    scc = set(front if front is not None else g.solve()["front"])
     assert q1 and q2 and not (set(q1) & set(q2))
     assert set(q1) <= scc and set(q2) <= scc
     a2 = [v in set(q2) for v in range(g.n)]
@@ -162,7 +161,7 @@ def test_tiered_8_full_search_counts():
 BIG = json.load(open(os.path.join(GOLDEN, "golden_big.json")))
 
 
-@pytest.mark.parametrize("name", sorted(BIG))
+@pytest.mark.parametrize("name", sorted(n for n in BIG if n.startswith("two_tier_")))
 def test_big_two_tier_counts(name):
     # bench-size workloads; golden counts from the oracle's full CPU search
     # (tests/golden/make_golden.py --big: ~70 s and ~450 s single-threaded)
@@ -171,6 +170,30 @@ def test_big_two_tier_counts(name):
         d = qa.FBAS(fbas_gen.two_tier(int(k), int(n))).solve_stats(jit=jit)
         g = BIG[name]
         assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (g["verdict"], g["nodes"], g["evals"], g["minq"])
+
+
+def test_planted_deep_exact():
+    # BASELINE configs[4]: 512 validators, the first witness 1.90M nodes into a 4.75M-node
+    # tree; golden counts and witness from the oracle (make_golden.py --big planted_deep)
+    text = fbas_gen.planted_deep(8, 512)
+    g = BIG["planted_deep_8_512"]
+    for jit in (1, 2):
+        d = qa.FBAS(text).solve_stats(jit=jit)
+        _cmp(d, g, "planted_deep_8_512")
+    _validate_witness(text, d["q1"], d["q2"], g["front"])
+    d = qa.FBAS(fbas_gen.planted_deep(8, 512, plant=False)).solve_stats(jit=2)
+    _cmp(d, BIG["planted_deep_8_512_intact"], "planted_deep_8_512_intact")
+
+
+@pytest.mark.parametrize("world,target,batch", [(4, 512, 8), (3, 100, 64)])
+def test_planted_deep_dealt(world, target, batch):
+    # the deep witness through the multi-engine path: preorder-filtered totals and the
+    # preorder-first witness equal the single-engine (and oracle) answer
+    g = BIG["planted_deep_8_512"]
+    d = _dealt_search(fbas_gen.planted_deep(8, 512), world, target, batch)
+    assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (g["verdict"], g["nodes"], g["evals"] - g["scc_evals"],
+                                                                 g["minq"])
+    assert (d["q1"], d["q2"]) == (g["q1"], g["q2"])
 
 
 def test_large_scc_multiword_masks():

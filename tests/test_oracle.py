@@ -159,3 +159,21 @@ def test_threshold_zero_quirk():
     g = Oracle().load(json.dumps(nodes))
     assert g.slice(0, [True, False]) is True
     assert g.slice(0, [True, True]) is False
+
+
+def test_planted_deep_construction():
+    # BASELINE configs[4] generator: the golden witness (oracle, make_golden.py --big) is a
+    # pair of disjoint quorums of the SCC, and plant=False breaks exactly that pair (HB
+    # members then need b0, which lies in the A-side quorum)
+    big = json.load(open(os.path.join(GOLDEN, "golden_big.json")))
+    g = big["planted_deep_8_512"]
+    assert (g["verdict"], g["nodes"]) == (False, 1895551)
+    assert big["planted_deep_8_512_intact"]["verdict"] and big["planted_deep_8_512_intact"]["nodes"] == 4750447
+    q1, q2, scc = set(g["q1"]), set(g["q2"]), set(g["front"])
+    assert q1 and q2 and not (q1 & q2) and q1 <= scc and q2 <= scc and len(scc) == 32
+    for plant in (True, False):
+        o = Oracle().load(fbas_gen.planted_deep(8, 512, plant=plant))
+        a1 = [v in q1 for v in range(o.n)]
+        a2 = [v in q2 for v in range(o.n)]
+        assert all(o.slice(v, a2) for v in q2)
+        assert all(o.slice(v, a1) for v in q1) == plant

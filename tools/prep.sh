@@ -8,6 +8,7 @@ make -C quorum_intersection_amd/csrc -j8 >> /tmp/qi_build.log 2>&1 || { grep -A5
 python3 -c "
 import quorum_intersection_amd as qa
 from quorum_intersection_amd import fbas_gen
-fb = qa.FBAS(fbas_gen.two_tier(10, 256), device=0)
-print('jit precompile ms', round(fb.jit_precompile(), 1))
+for t in (fbas_gen.two_tier(10, 256), fbas_gen.planted_deep(8, 512), fbas_gen.planted_deep(8, 512, plant=False)):
+    fb = qa.FBAS(t, device=0)
+    print('jit precompile ms', round(fb.jit_precompile(), 1))
 "
