@@ -110,6 +110,7 @@ class DeviceSearch(SearchBackend):
         keep = None
         if n:
             keep = torch.empty(n * self.unit_bytes, dtype=torch.uint8, device=self.data_device)
+            _settle(keep)
             self.export(n, keep)
         self._c.check(self.L.qi_search_restart(self.h))
         self.clear()
@@ -282,6 +283,15 @@ def _to_comm(t: torch.Tensor, device) -> torch.Tensor:
     return t if t.device == torch.device(device) else t.to(device)
 
 
+def _settle(t: torch.Tensor) -> None:
+    """The engine copies units on its own non-blocking HIP stream, which is not ordered
+    after torch's current stream: a blocking RCCL collective only makes the *current
+    stream* wait for its result, and a fresh caching-allocator block may still be in use
+    by work queued there.  Drain the current stream before the engine touches `t`."""
+    if t.is_cuda:
+        torch.cuda.current_stream(t.device).synchronize()
+
+
 def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int = 1 << 17,
                        rebalance: bool = True, min_move: int = 64, seed_units: int = 0) -> DistResult:
     """Run one full search across the ranks of `group`; every rank returns the result."""
@@ -307,12 +317,14 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
         if n:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             buf = _unit_buf(be, n, device)
+            _settle(buf)
             if rank == 0:
                 be.export(n, buf)
             cbuf = _to_comm(buf, device)
             dist.broadcast(cbuf, src, group=group)
             if cbuf is not buf:
                 buf.copy_(cbuf)
+            _settle(buf)
             be.import_(n, buf)
             be.keep_strided(rank, world)
     # (3) independent chains of launches; exchange sizes/best keys; rebalance surplus
@@ -332,6 +344,7 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
                 gdst = dist.get_global_rank(group, dst) if group is not None else dst
                 if rank == src:
                     buf = _unit_buf(be, cnt, device)
+                    _settle(buf)
                     be.export(cnt, buf)
                     dist.send(_to_comm(buf, device), gdst, group=group)
                 elif rank == dst:
@@ -340,6 +353,7 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
                     dist.recv(cbuf, gsrc, group=group)
                     if cbuf is not buf:
                         buf.copy_(cbuf)
+                    _settle(buf)
                     be.import_(cnt, buf)
                 moved += cnt
     # (4) preorder-exact totals against the global best witness
