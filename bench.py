@@ -264,6 +264,18 @@ def main():
     }
     if ttv_res["nodes"] != res.nodes or ttv_res["evals"] != evals_per_step:
         line["warning"] = "solve_stats and step-wise search disagree"
+    # the measured work must be the reference's exact tree: node count and verdict against
+    # the oracle's committed golden counts (tests/golden/golden_big.json) when they exist
+    gkey = {"two_tier": f"two_tier_{args.k_top}_{args.validators}",
+            "planted_deep": f"planted_deep_{args.k_top}_{args.validators}"}.get(args.workload)
+    gpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "golden_big.json")
+    golden = json.load(open(gpath)).get(gkey) if gkey and os.path.exists(gpath) else None
+    if golden is None:
+        line["golden"] = "no fixture for this workload"
+    else:
+        ok = golden["nodes"] == res.nodes and bool(golden["verdict"]) == bool(res.verdict)
+        line["golden"] = "match (nodes, verdict)" if ok else (
+            f"MISMATCH: nodes {res.nodes} vs {golden['nodes']}, verdict {res.verdict} vs {golden['verdict']}")
 
     if not args.no_cpu_baseline and world == 1:
         r = cpu_baseline(text, args.cpu_sample_nodes)
@@ -282,6 +294,8 @@ def main():
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if line["golden"].startswith("MISMATCH"):
+        raise SystemExit("bench: search result differs from the golden counts")
 
 
 if __name__ == "__main__":

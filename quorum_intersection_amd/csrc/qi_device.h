@@ -39,6 +39,8 @@ struct SearchConfig {
   uint32_t run_at = 4;           // run budget once the frontier holds >= run_at/8 of the resident lanes
   uint32_t steal_max = 0;        // per-lane entries taken from busy lanes per launch (bounds the log);
                                  // 0 = off: measured 4.6 vs 4.0 ms per search with 16 (QI_STEAL)
+  uint32_t coop_batch = 1;       // parked quorum leaves per cooperative phase (QI_COOP_BATCH; 1 = every
+                                 // iteration with a leaf runs the phase)
   uint32_t batch = 0;            // max chained launches per step() (0 = 64)
   uint32_t lookahead = 2;        // launches kept in flight beyond the one the host waits for
   bool keep_log = true;          // keep per-segment records for preorder-exact counts

@@ -406,6 +406,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_STEAL")) cfg_.steal_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_COOP_BATCH")) cfg_.coop_batch = (uint32_t)std::atoi(e);
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
     stream_ = acquire_stream(device_);
@@ -482,6 +483,7 @@ class SearchDeviceImpl : public SearchDevice {
     shm_ = (size_t)dev::search_lds_words<MW, SMAX>() * 4;
     shm_ = (shm_ + 15) / 16 * 16;
     jit_shm_ = shm_ + (size_t)(jit_smax_ - SMAX) * (2 * MW + 1) * 64 * 4;  // QI_JIT_SMAX (diagnostics)
+    if (jit_gstack()) jit_shm_ = (size_t)dev::search_lds_words<MW, SMAX, true>() * 4;
     jit_shm_ = (jit_shm_ + 15) / 16 * 16;
     HIP_CHECK(hipFuncSetAttribute((const void*)dev::search_kernel<MW, TW, SMAX>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
@@ -612,6 +614,8 @@ class SearchDeviceImpl : public SearchDevice {
       a.coop_slot = sl;
       a.coop_slot_log2 = lg;
     }
+    a.gstack = gstack_;
+    a.coop_batch = std::max(1u, cfg_.coop_batch);
     a.has_best = has_best_ ? 1u : 0u;
     a.best_depth = best_depth_;
     for (int w = 0; w < 8; ++w) a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
@@ -975,7 +979,7 @@ class SearchDeviceImpl : public SearchDevice {
 
   void start_jit() {
     jit_state_.store(1);
-    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3);
+    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3, jit_gstack());
     jit_thread_ = std::thread([this, src]() {
       std::vector<char> code = jit_compile(src, &jit_log_);
       jit_code_ = std::move(code);
@@ -996,10 +1000,17 @@ class SearchDeviceImpl : public SearchDevice {
     jit_state_.store(4);
     if (!cfg_.max_blocks) {
       int nb = 0;
-      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jit_fn_, 64, jit_shm_) == hipSuccess && nb > 0)
+      if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, jit_fn_, 64, jit_shm_) == hipSuccess && nb > 0) {
+        if (const char* e = std::getenv("QI_JIT_WAVES")) nb = std::max(1, std::min(nb, std::atoi(e)));  // diagnostics
         max_blocks_ = cus_ * (uint32_t)nb;
+      }
+    }
+    if (jit_gstack()) {  // one stack region per resident block: [64 lanes][SMAX][2MW+1]
+      const size_t words = (size_t)max_blocks_ * 64u * (size_t)jit_smax_ * (2 * MW + 1);
+      keep(gstack_ = dalloc<uint32_t>(words));
     }
   }
+  uint32_t* gstack_ = nullptr;
 };
 
 }  // namespace
@@ -1021,7 +1032,7 @@ bool jit_precompile(const LocalFlat& f, std::string* log) {
   else if (mw <= 8 && tw <= 8) { MW = 8; TW = 8; SMAX = 8; }
   else return false;
   if (!jit_eligible(f)) return false;
-  return !jit_compile(jit_source(f, MW, TW, SMAX), log).empty();
+  return !jit_compile(jit_source(f, MW, TW, SMAX, false, jit_gstack()), log).empty();
 }
 
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg) {

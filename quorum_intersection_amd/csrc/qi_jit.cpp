@@ -63,9 +63,18 @@ bool jit_eligible(const LocalFlat& f) {
   return f.T <= 1024 && f.G <= 1024 && f.extra_src.size() <= 4096 && f.grp_extra.size() <= 4096 * 8;
 }
 
-std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps) {
+bool jit_gstack() {
+  static const bool on = [] {
+    const char* e = std::getenv("QI_GSTACK");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return on;
+}
+
+std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps, bool gstack) {
   std::ostringstream o;
   if (stamps) o << "#define QI_STAMPS 1\n";
+  if (gstack) o << "#define QI_GSTACK 1\n";
   // diagnostics only (never set for measurements): QI_JIT_DEFINES="A,B=2" adds #defines,
   // e.g. the QI_ABL_* ablations of qi_search_kernel.h that repeat one section
   if (const char* e = std::getenv("QI_JIT_DEFINES")) {

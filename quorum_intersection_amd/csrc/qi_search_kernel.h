@@ -284,6 +284,8 @@ struct SearchArgs {
   uint32_t best_depth;
   uint32_t best_key[8];
   uint32_t diag;                 // 0; opaque to the compiler (keeps QI_ABL_* repeats alive)
+  uint32_t coop_batch;           // parked quorum leaves that trigger a cooperative phase
+  uint32_t* gstack;              // QI_GSTACK builds: [blocks][64 lanes][SMAX][2MW+1] DFS stacks
 };
 
 enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u };
@@ -341,10 +343,12 @@ __device__ __forceinline__ uint32_t reserve(uint32_t n, uint32_t* counter, uint3
   return base + pre;
 }
 
-// LDS words of one search wavefront (search_body's carve-up below).
-template <int MW, int SMAX>
+// LDS words of one search wavefront (search_body's carve-up below).  QI_GSTACK keeps the
+// DFS stack in global memory instead (L1/L2-resident, per-lane contiguous): the LDS then
+// no longer caps the resident waves per CU (7 at MW = 1), registers do.
+template <int MW, int SMAX, bool GSTACK = false>
 constexpr int search_lds_words() {
-  return SMAX * (2 * MW + 1) * WAVE             // DFS stack below the top entry
+  return (GSTACK ? 0 : SMAX * (2 * MW + 1) * WAVE)  // DFS stack below the top entry
          + 2 * MW * WAVE                        // co_NE, co_VIS
          + (MW + 1) * WAVE                      // co_D, co_OWN
          + ((UnitLayout<MW>::DMAX + 3) / 4) * WAVE;  // D order
@@ -391,8 +395,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   constexpr bool PREFETCH = UW <= 20;
   constexpr int FW = PREFETCH ? UW : 4;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+#ifdef QI_GSTACK
+  uint32_t* const st = a.gstack + (size_t)blockIdx.x * (SMAX * SE * WAVE);  // [64][SMAX][SE]
+  uint32_t* co_NE = lds;                                        // [MW][64] per pending rank
+#else
   uint32_t* st = lds;                                          // [SMAX][SE][64]
   uint32_t* co_NE = st + SMAX * SE * WAVE;                      // [MW][64] per pending rank
+#endif
   uint32_t* co_VIS = co_NE + MW * WAVE;                         // [MW][64] per pending rank
   uint32_t* co_D = co_VIS + MW * WAVE;                          // [MW][64] pending owners' D
   uint32_t* co_OWN = co_D + MW * WAVE;                          // [64] owner lane | dlen << 8
@@ -440,7 +449,12 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   }
   uint32_t* const records = a.records + (size_t)log_base * RL::WORDS;
   const uint32_t budget = ((uint64_t)n_in * 8u >= (uint64_t)gridDim.x * WAVE * a.run_at) ? a.run_budget : a.grow_budget;
-#define ST_(lvl, w) st[((lvl) * SE + (w)) * WAVE + lane]
+#ifdef QI_GSTACK
+#define ST_IDX(lvl, w, ln) ((((ln) * SMAX) + (lvl)) * SE + (w))
+#else
+#define ST_IDX(lvl, w, ln) (((lvl) * SE + (w)) * WAVE + (ln))
+#endif
+#define ST_(lvl, w) st[ST_IDX(lvl, w, lane)]
 #define DOW_(w) dow[(w) * WAVE + lane]
   // byte i of this lane's D order (ds_write_b8 into the packed word)
   auto set_ord = [&](uint32_t i, uint32_t v) {
@@ -453,6 +467,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   for (int w = 0; w < MW; ++w) T[w] = D[w] = K[w] = 0;
   uint32_t depth = 0, dlen = 0;
   bool has = false, done = false;
+  bool park = false;  // the node is a quorum leaf waiting for the next cooperative phase
   // top of the DFS stack in registers; `nst` entries below it in LDS (circular from sbase_)
   uint32_t tT[MW], tD[MW], tpk = 0;
 #pragma unroll
@@ -792,17 +807,19 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           }
           const uint32_t xbase = xpool_next;
           xpool_next += np;
+#ifdef QI_GSTACK
+          __threadfence_block();  // the donors' global stack stores, visible to the receivers
+#endif
           if (idle && ri < np) {  // receiver: the entry becomes its unit
             const uint32_t own = co_OWN[ri];
             const uint32_t dl = own & 63u, pos = own >> 8;
-            const uint32_t* ent = st + (size_t)pos * SE * WAVE + dl;
 #pragma unroll
             for (int w = 0; w < MW; ++w) {
-              T[w] = ent[w * WAVE];
-              D[w] = ent[(MW + w) * WAVE];
+              T[w] = st[ST_IDX(pos, w, dl)];
+              D[w] = st[ST_IDX(pos, MW + w, dl)];
               K[w] = co_D[w * WAVE + ri];
             }
-            const uint32_t pk = ent[2 * MW * WAVE];
+            const uint32_t pk = st[ST_IDX(pos, 2 * MW, dl)];
             const uint32_t b = pk & 255u, de = (pk >> 8) & 511u, dle = pk >> 17;
             key_prefix_bit<MW>(K, de);
             depth = de + 1;
@@ -868,7 +885,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     QI_STAMP(1);  // claims + polls
     // ---- (3) budget exhausted: spill current node, top, stack and claimed unit ---------
     {
-      const bool spill = (has && (steps >= limit || evictions >= a.evict_max)) ||
+      const bool spill = (has && !park && (steps >= limit || evictions >= a.evict_max)) ||
                          (!has && fpend && steps >= limit);
       if (__any(spill)) {
         uint32_t total = 0;
@@ -894,8 +911,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // ---- (4) one search node per active lane (cpp:258-345) ---------------------------
     ++wave_iters;
     bool pending = false;
-    bool active = has;
-    if (has) {
+    bool active = has && !park;
+    if (active) {
       ++steps;
       ++seg_count;
       uint32_t any = 0;
@@ -1033,14 +1050,18 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
     }
-    const uint64_t pm = __ballot(pending);
+    // Quorum leaves park until coop_batch of them are waiting (one phase then serves up
+    // to 64 / S owners per pass) or no lane of the wave has a node left to search.
+    park = park || pending;
+    const uint64_t pk_m = __ballot(park);
+    const uint64_t pm = (pk_m && ((uint32_t)__popcll(pk_m) >= a.coop_batch || !__any(has && !park))) ? pk_m : 0ull;
     if (pm) {
       ++coop_phases;
       const uint32_t npend = (uint32_t)__popcll(pm);
       const uint32_t r = rank_in(pm);
       const uint32_t S = a.coop_slot, lgS = a.coop_slot_log2;
       const uint32_t P = (uint32_t)WAVE >> lgS;  // owners per pass
-      if (pending) {  // owner slot r: results zeroed, D / lane / |D| published
+      if (park) {  // owner slot r: results zeroed, D / lane / |D| published
 #pragma unroll
         for (int w = 0; w < MW; ++w) {
           co_NE[w * WAVE + r] = 0u;
@@ -1092,7 +1113,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
       __syncthreads();
-      if (pending) {
+      if (park) {
+        park = false;
         uint32_t ne_any = 0, vis_any = 0;
         uint32_t NE[MW], VIS[MW];
 #pragma unroll
@@ -1225,6 +1247,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     }
   }
 #undef ST_
+#undef ST_IDX
 #undef DOW_
 }
 

@@ -435,3 +435,17 @@ def test_stealing_exact(name, monkeypatch):
         assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"], r["evals"], r["minq"])
         if not r["verdict"]:
             assert d["q1"] == r["q1"] and d["q2"] == r["q2"]
+
+
+# ---- parked quorum leaves (QI_COOP_BATCH = leaves per cooperative phase; default 1) -------
+@pytest.mark.parametrize("batch", ["2", "4"])
+@pytest.mark.parametrize("name", ["tiered_6", "broken", "planted_5_96", "tiered_5_shuffled"])
+def test_coop_batch_exact(name, batch, monkeypatch):
+    monkeypatch.setenv("QI_COOP_BATCH", batch)
+    text = _text_for(name)
+    r = GOLD[name] if name in GOLD else Oracle().load(text).solve()
+    for jit in (1, 2):
+        d = qa.FBAS(text).solve_stats(jit=jit, grow_budget=2, run_budget=64)
+        assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"], r["evals"], r["minq"])
+        if not r["verdict"]:
+            assert d["q1"] == r["q1"] and d["q2"] == r["q2"]
