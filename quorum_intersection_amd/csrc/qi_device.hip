@@ -850,9 +850,8 @@ class SearchDeviceImpl : public SearchDevice {
     for (auto& c : log_) c.used = 0;
     DeviceGuard dg(device_);
     HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * dev::TOT_SHARDS * sizeof(unsigned long long), stream_));
-    unsigned long long inf = ~0ull;
-    HIP_CHECK(hipMemcpyAsync(best64_, &inf, 8, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    // no-witness best key; stream-ordered before every later launch, no host round trip
+    HIP_CHECK(hipMemsetAsync(best64_, 0xFF, 8, stream_));
     has_best_ = false;
     has_local_best_ = false;
     sum_ms_ = 0;

@@ -360,12 +360,12 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
     sizes, keys = _gather_state(be, device, group) if world > 1 else ([0], [be.local_best()])
     best = best_of(keys)
     loc = be.reduce(best)
-    vec = torch.tensor([loc["nodes"], loc["evals"], loc["minq"], loc["zero_fallback"], loc["rounds"], launches,
-                        loc.get("units", 0), loc.get("wave_iters", 0), loc.get("coop_phases", 0)],
-                       dtype=torch.int64, device=device)
-    if world > 1:
+    tot = [int(loc["nodes"]), int(loc["evals"]), int(loc["minq"]), int(loc["zero_fallback"]), int(loc["rounds"]),
+           launches, int(loc.get("units", 0)), int(loc.get("wave_iters", 0)), int(loc.get("coop_phases", 0))]
+    if world > 1:  # one process: no device round trip for the totals
+        vec = torch.tensor(tot, dtype=torch.int64, device=device)
         dist.all_reduce(vec, group=group)
-    tot = [int(x) for x in vec.tolist()]
+        tot = [int(x) for x in vec.tolist()]
     q1: List[int] = []
     q2: List[int] = []
     if best is not None:
