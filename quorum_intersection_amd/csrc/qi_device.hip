@@ -337,6 +337,7 @@ class GfpDeviceImpl : public GfpDevice {
     for (auto* p : bufs_) (void)hipFree((void*)p);
     (void)hipFree(rounds_);
     (void)hipFree(io_);
+    if (hio_) (void)hipHostFree(hio_);
     (void)hipEventDestroy(e0_);
     (void)hipEventDestroy(e1_);
     release_stream(device_, stream_);
@@ -347,14 +348,18 @@ class GfpDeviceImpl : public GfpDevice {
     const size_t per = (size_t)count * d_.words;
     if (io_cap_ < per) {
       (void)hipFree(io_);
+      if (hio_) (void)hipHostFree(hio_);
       io_ = dalloc<unsigned long long>(3 * per);
+      HIP_CHECK(hipHostMalloc((void**)&hio_, 3 * per * 8, hipHostMallocDefault));
       io_cap_ = per;
     }
     unsigned long long* dn = io_;
     unsigned long long* da = io_ + per;
     unsigned long long* dout = io_ + 2 * per;
-    HIP_CHECK(hipMemcpyAsync(dn, nodes, per * 8, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipMemcpyAsync(da, avail, per * 8, hipMemcpyHostToDevice, stream_));
+    // both inputs through one pinned staging buffer: one DMA each way per batch
+    std::memcpy(hio_, nodes, per * 8);
+    std::memcpy(hio_ + per, avail, per * 8);
+    HIP_CHECK(hipMemcpyAsync(dn, hio_, 2 * per * 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(rounds_, 0, 8, stream_));
     const size_t shm = (size_t)d_.words * 16 + ((d_.T + 15) / 16) * 16;
     if (shm > 160 * 1024) throw Error(QI_ERR_UNSUPPORTED, "gfp_batch: FBAS too large for LDS staging");
@@ -362,8 +367,9 @@ class GfpDeviceImpl : public GfpDevice {
     hipLaunchKernelGGL(dev::gfp_batch_kernel, dim3(count), dim3(64), shm, stream_, d_, dn, da, count, dout, rounds_);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipEventRecord(e1_, stream_));
-    HIP_CHECK(hipMemcpyAsync(out, dout, per * 8, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(hio_ + 2 * per, dout, per * 8, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    std::memcpy(out, hio_ + 2 * per, per * 8);
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, e0_, e1_));
     last_ms_ = ms;
@@ -378,6 +384,7 @@ class GfpDeviceImpl : public GfpDevice {
   std::vector<const uint32_t*> bufs_;
   unsigned long long* rounds_ = nullptr;
   unsigned long long* io_ = nullptr;
+  unsigned long long* hio_ = nullptr;  // pinned staging: nodes, avail, out
   size_t io_cap_ = 0;
   double last_ms_ = 0;
 };
