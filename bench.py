@@ -51,9 +51,20 @@ def ops_per_best(sh):
     return sh["groups"] * (4 * w + 3)
 
 
-def cpu_baseline(text: str, sample_nodes: int) -> dict:
-    """The oracle (oracle/qi_oracle.cpp, -O3, one pinned core) on the first
-    `sample_nodes` search nodes of the same workload, in a child process."""
+def host_cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(text: str, sample_nodes: int, so: str | None = None) -> dict:
+    """The oracle (oracle/qi_oracle.cpp, -O3 unless `so` names another build of it, one
+    pinned core) on the first `sample_nodes` search nodes of the same workload, in a
+    child process."""
     code = (
         "import os, sys, json; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
         "os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})\n"
@@ -62,7 +73,11 @@ def cpu_baseline(text: str, sample_nodes: int) -> dict:
         "r = Oracle().load(t).solve(budget=%d)\n"
         "print(json.dumps(r))\n" % (ROOT, os.path.join(ROOT, "tests"), sample_nodes)
     )
-    out = subprocess.run([sys.executable, "-c", code], input=text, capture_output=True, text=True, check=True)
+    env = dict(os.environ)
+    if so:
+        env["QI_ORACLE_SO"] = so
+    out = subprocess.run([sys.executable, "-c", code], input=text, capture_output=True, text=True, check=True,
+                         env=env)
     r = json.loads(out.stdout.strip().splitlines()[-1])
     return r
 
@@ -278,8 +293,14 @@ def main():
             f"MISMATCH: nodes {res.nodes} vs {golden['nodes']}, verdict {res.verdict} vs {golden['verdict']}")
 
     if not args.no_cpu_baseline and world == 1:
-        r = cpu_baseline(text, args.cpu_sample_nodes)
+        # median of 3 runs of the -O3 oracle, plus the -O0 build of the same
+        # source on a 1/16 sample: the reference's documented build sets no optimisation
+        runs = sorted((cpu_baseline(text, args.cpu_sample_nodes) for _ in range(3)),
+                      key=lambda x: x["evals"] / x["seconds"])
+        r = runs[1]
         cpu_evals_s = r["evals"] / r["seconds"]
+        o0_so = os.path.join(ROOT, "oracle", "_build", "libqi_oracle_O0.so")
+        r0 = cpu_baseline(text, max(args.cpu_sample_nodes // 16, 1), so=o0_so) if os.path.exists(o0_so) else None
         line["cpu_baseline"] = {
             "value": cpu_evals_s,
             "unit": "fixpoint-evals/s",
@@ -289,6 +310,14 @@ def main():
                        f"({r['evals']:,} evals incl. {r['scc_evals']} per-SCC checks) of the same workload "
                        f"in {r['seconds']:.1f} s"),
             "time_to_verdict_est_s": evals_per_step / cpu_evals_s,
+            "runs_evals_s": [x["evals"] / x["seconds"] for x in runs],
+            "statistic": "median of 3",
+            "host_cpu": host_cpu_model(),
+            "host_nproc": os.cpu_count(),
+            "reference_build_O0": None if r0 is None else {
+                "value": r0["evals"] / r0["seconds"],
+                "sample": f"same oracle source at -O0, first {r0['nodes']:,} search nodes in {r0['seconds']:.1f} s",
+            },
         }
         line["speedup_vs_cpu"] = value / cpu_evals_s
     print(json.dumps(line), flush=True)

@@ -13,7 +13,9 @@ from typing import Dict, List, Optional
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "libqi_oracle.so")
+# QI_ORACLE_SO: another build of the same oracle source (bench.py times the -O0 build, the
+# reference's documented CMake build having no build type)
+ORACLE_SO = os.environ.get("QI_ORACLE_SO") or os.path.join(ORACLE_DIR, "_build", "libqi_oracle.so")
 ORACLE_BIN = os.path.join(ORACLE_DIR, "_build", "qi_oracle")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 FIXTURES = ["correct", "broken", "correct_trivial", "broken_trivial"]
