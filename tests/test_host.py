@@ -164,3 +164,11 @@ def test_specialised_kernel_sources_compile(case):
     }
     ms = qa.FBAS(texts[case]).jit_precompile()
     assert ms >= 0
+
+
+def test_bench_default_workloads_have_golden_counts():
+    # bench.py checks every measured search against these (node count, verdict)
+    import json
+    big = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden_big.json")))
+    for key in ("two_tier_10_256", "planted_deep_8_512"):
+        assert key in big and big[key]["nodes"] > 0 and "verdict" in big[key]
