@@ -378,6 +378,13 @@ constexpr int search_lds_words() {
 #ifndef QI_INSTALL_AGE
 #define QI_INSTALL_AGE 0
 #endif
+// iterations between polls of the global queue head and the device-side best key
+#ifndef QI_POLL_MASK
+#define QI_POLL_MASK 31
+#endif
+#ifndef QI_POLL_ASYNC
+#define QI_POLL_ASYNC 1
+#endif
 
 template <int MW, int TW, int SMAX, class EV>
 __device__ __forceinline__ void search_body(const SearchArgs& a) {
@@ -506,6 +513,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   uint64_t best64 = ~0ull;
+  uint32_t poll_h = 0;     // QI_POLL_ASYNC: lane 0's pre-issued poll loads (the first poll,
+  uint64_t poll_b = ~0ull;  // at iteration 0, reads the ones issued here)
+#if QI_POLL_ASYNC
+  if (lane == 0) {
+    poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    poll_b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#endif
 
   auto load_unit = [&](uint32_t idx) {  // issue the loads (consumed at install)
     if constexpr (PREFETCH) {
@@ -867,13 +882,28 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // to claim anywhere, every lane gets a short grace period and then spills: the next
     // launch spreads the remaining subtrees over all lanes instead of letting a few lanes
     // grind through deep subtrees while the rest idle.
-    if ((iter++ & 31u) == 0u) {
+#if QI_POLL_ASYNC
+    // the loads are issued one iteration before the poll that reads them, so their latency
+    // hides behind that iteration (the values are at most one iteration older)
+    if (((iter + 1u) & (uint32_t)QI_POLL_MASK) == 0u && lane == 0) {
+      poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      poll_b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
+    if ((iter++ & (uint32_t)QI_POLL_MASK) == 0u) {
       uint32_t h = 0;
       uint64_t b = ~0ull;
+#if QI_POLL_ASYNC
+      if (lane == 0) {
+        h = static_end + poll_h;
+        b = poll_b;
+      }
+#else
       if (lane == 0) {
         h = static_end + __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+#endif
       h = lane0(h);
       best64 = lane0(b);
       if (!dry && h >= n_in) {
