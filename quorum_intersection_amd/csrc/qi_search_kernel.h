@@ -382,6 +382,22 @@ constexpr int search_lds_words() {
 #ifndef QI_POLL_MASK
 #define QI_POLL_MASK 31
 #endif
+// The cooperative phase's LDS hand-offs stay inside one wavefront (blockDim == 64), whose
+// LDS operations complete in issue order: QI_COOP_WAVESYNC orders them with a wave-level
+// barrier instead of a workgroup barrier (whose fences also wait for outstanding global
+// memory operations).
+#ifndef QI_COOP_WAVESYNC
+#define QI_COOP_WAVESYNC 0
+#endif
+#if QI_COOP_WAVESYNC
+#define QI_COOP_SYNC()                                       \
+  do {                                                       \
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   \
+    __builtin_amdgcn_wave_barrier();                         \
+  } while (0)
+#else
+#define QI_COOP_SYNC() __syncthreads()
+#endif
 #ifndef QI_POLL_ASYNC
 #define QI_POLL_ASYNC 1
 #endif
@@ -1100,7 +1116,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
         co_OWN[r] = lane | (dlen << 8);
       }
-      __syncthreads();
+      QI_COOP_SYNC();
       for (uint32_t q0 = 0; q0 < npend; q0 += P) {
         const uint32_t oi = q0 + (lane >> lgS);
         const uint32_t oc = min(oi, (uint32_t)WAVE - 1u);  // slots >= npend: stale, masked by `act`
@@ -1142,7 +1158,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           if (c0 + S > a.half_m) break;
         }
       }
-      __syncthreads();
+      QI_COOP_SYNC();
       if (park) {
         park = false;
         uint32_t ne_any = 0, vis_any = 0;
@@ -1165,7 +1181,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           seg_evals += 2u + pos;  // cpp:184 + (pos+1) x cpp:192
         }
       }
-      __syncthreads();
+      QI_COOP_SYNC();
     }
     QI_STAMP(5);  // quorum-leaf phase
     if (pm) {  // lanes freed by the cooperative phase
