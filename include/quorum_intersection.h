@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define QI_ABI_VERSION 2
+#define QI_ABI_VERSION 3
 
 enum {
   QI_OK = 0,
@@ -88,6 +88,13 @@ typedef struct {
                               3 = 2 + diagnostic section stamps (not for measurement) */
   uint32_t batch;          /* 0 = default: search launches chained on the device per host
                               synchronisation (each reads its input count from the previous) */
+  uint32_t engines;        /* search shards: 0 = one per selected device.  Shards split the
+                              search tree by branch prefix (one host thread + HIP stream each,
+                              round-robin over the devices); >1 on one device runs the same
+                              sharded code path on one GPU */
+  uint32_t device_mask;    /* HIP devices of the search, bit d = device d; 0 = the qi_fbas
+                              device only.  Units move between devices over xGMI
+                              (hipMemcpyPeerAsync) */
 } qi_solve_opts;
 
 typedef struct {
@@ -109,10 +116,14 @@ typedef struct {
   double t_search_ms;      /* search, host wall */
   double t_kernel_ms;      /* search kernels, HIP events */
   uint32_t nonmonotone;    /* 1 if the searched SCC has threshold-0 quorum sets: the
-                              reference's fixpoints then depend on its sweep order, which
-                              at cpp:301 is libstdc++ unordered_set iteration order; the
-                              device search uses Jacobi rounds there (parity unpinned) */
+                              reference's fixpoints then depend on its sweep orders (D in
+                              branch order, toRemove in libstdc++ unordered_set order); the
+                              search then runs the order-exact kernel (same counts) */
   uint32_t jit_launches;   /* launches that ran the run-time specialised kernel */
+  uint32_t engines;        /* search shards that ran */
+  uint32_t devices;        /* distinct HIP devices they ran on */
+  uint64_t units_moved;    /* frontier units handed between shards (rebalancing) */
+  double t_device_init_ms; /* HIP runtime / device contexts of the search devices, host wall */
 } qi_solve_result;
 
 /* q1, q2: caller buffers of n_vertices entries (may be NULL).  q1 = disjoint quorum
@@ -214,6 +225,14 @@ double qi_search_kernel_ms(const qi_search* s);
  * returns 1 if the next launch will use the specialised kernel. */
 int qi_search_wait_jit(qi_search* s);
 int qi_search_shape(const qi_search* s, qi_shape* out);
+
+/* The search's reproduction of libstdc++ std::unordered_set<size_t> iteration order
+ * (toRemove at cpp:308/331 is that order; it decides the Gauss-Seidel sweeps on
+ * threshold-0 SCCs).  keys[v] = global vertex index of local vertex v (n_keys <= 256);
+ * the set is built by inserting keys[seq[0]], keys[seq[1]], ... (repeats ignored);
+ * out[0..*n_out) = local vertices in iteration order.  Host only, no GPU needed. */
+int qi_hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint32_t* seq, uint32_t n_seq,
+                            uint32_t* out, uint32_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -362,6 +362,7 @@ struct Ctx {
   uint64_t zero_fallback = 0;  // findBestNode returned *quorum.begin() (no in-edges)
   uint64_t budget = 0;      // 0 = unlimited
   bool aborted = false;
+  uint64_t depth = 0, max_depth = 0;  // recursion depth of iterateMinimalQuorums (root = 0)
 };
 
 // containsQuorumSlice (cpp:90-138)
@@ -458,8 +459,18 @@ static NodeIx findBestNode(Ctx& ctx, const std::vector<NodeIx>& quorum, const st
 using Visitor = std::function<bool(const std::vector<NodeIx>&)>;
 
 // iterateMinimalQuorums (cpp:252-346)
+static bool iterateMinimalQuorumsBody(Ctx& ctx, std::vector<NodeIx> toRemove, std::vector<NodeIx> dontRemove,
+                                      const Graph& g, const Visitor& visitor, const Visitor& currentVisitor);
 static bool iterateMinimalQuorums(Ctx& ctx, std::vector<NodeIx> toRemove, std::vector<NodeIx> dontRemove,
                                   const Graph& g, const Visitor& visitor, const Visitor& currentVisitor) {
+  ctx.max_depth = std::max(ctx.max_depth, ctx.depth);
+  ++ctx.depth;
+  const bool r = iterateMinimalQuorumsBody(ctx, std::move(toRemove), std::move(dontRemove), g, visitor, currentVisitor);
+  --ctx.depth;
+  return r;
+}
+static bool iterateMinimalQuorumsBody(Ctx& ctx, std::vector<NodeIx> toRemove, std::vector<NodeIx> dontRemove,
+                                      const Graph& g, const Visitor& visitor, const Visitor& currentVisitor) {
   if (ctx.budget && ctx.nodes >= ctx.budget) {
     ctx.aborted = true;
     return true;  // unwind (instrumentation only)
@@ -836,6 +847,7 @@ char* qio_solve(void* h, int tiebreak, uint64_t seed, uint64_t node_budget) {
   s += ",\"scc_evals\":" + std::to_string(ctx.scc_evals);
   s += ",\"minq\":" + std::to_string(ctx.minq);
   s += ",\"zero_fallback\":" + std::to_string(ctx.zero_fallback);
+  s += ",\"max_depth\":" + std::to_string(ctx.max_depth);
   s += ",\"q1\":" + qio::idxList(info.q1);
   s += ",\"q2\":" + qio::idxList(info.q2);
   char buf[64];
@@ -856,6 +868,29 @@ char* qio_solve_text(void* h, int verbose, int graphviz) {
   auto info = qio::solve(ctx, g, out, verbose != 0, graphviz != 0);
   out << info.verdict << std::endl;
   return strdup(out.str().c_str());
+}
+
+// Iteration order of std::unordered_set<size_t> built like cpp:308 from the keys of
+// seq[0..n_seq) (keys[v] = global index of local vertex v); out = local vertices.
+uint64_t qio_hash_order(const uint32_t* keys, uint32_t n_keys, const uint32_t* seq, uint32_t n_seq, uint32_t* out) {
+  std::vector<size_t> v;
+  std::unordered_map<size_t, uint32_t> local;
+  for (uint32_t i = 0; i < n_keys; ++i) local[keys[i]] = i;
+  for (uint32_t i = 0; i < n_seq; ++i) v.push_back(keys[seq[i]]);
+  std::unordered_set<size_t> s(v.begin(), v.end());
+  uint64_t n = 0;
+  for (size_t k : s) out[n++] = local[k];
+  return n;
+}
+
+// bucket_count() of that set after k distinct insertions, k = 1..nmax
+void qio_hash_bucket_counts(uint32_t nmax, uint64_t* out) {
+  std::vector<size_t> v;
+  for (uint32_t k = 1; k <= nmax; ++k) {
+    v.push_back(k * 7 + 3);
+    std::unordered_set<size_t> s(v.begin(), v.end());
+    out[k - 1] = s.bucket_count();
+  }
 }
 
 char* qio_pagerank_text(void* h, float m, float conv, uint64_t iters) {

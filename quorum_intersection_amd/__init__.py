@@ -125,10 +125,12 @@ class FBAS:
 
     # ---- device: solve / search -------------------------------------------------------
     def solve_stats(self, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0, jit: int = 0,
-                    batch: int = 0) -> Dict:
+                    batch: int = 0, engines: int = 0, device_mask: int = 0) -> Dict:
         """jit: 0 auto (specialised kernel compiled in the background for long searches),
-        1 table-interpreting kernel only, 2 specialised kernel from the first launch."""
-        opts = _capi.SolveOpts(0, grow_budget, run_budget, max_blocks, jit, batch)
+        1 table-interpreting kernel only, 2 specialised kernel from the first launch.
+        engines / device_mask: sharded search over several engines (one host thread and
+        HIP stream each) on the devices of device_mask (0 = this FBAS's device)."""
+        opts = _capi.SolveOpts(0, grow_budget, run_budget, max_blocks, jit, batch, engines, device_mask)
         res = _capi.SolveResult()
         q1 = np.zeros(max(self.n, 1), dtype=np.uint32)
         q2 = np.zeros(max(self.n, 1), dtype=np.uint32)

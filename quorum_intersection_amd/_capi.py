@@ -29,7 +29,7 @@ class QIError(RuntimeError):
 
 class SolveOpts(ctypes.Structure):
     _fields_ = [("tiebreak", c_uint32), ("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32),
-                ("jit", c_uint32), ("batch", c_uint32)]
+                ("jit", c_uint32), ("batch", c_uint32), ("engines", c_uint32), ("device_mask", c_uint32)]
 
 
 class SolveResult(ctypes.Structure):
@@ -54,6 +54,10 @@ class SolveResult(ctypes.Structure):
         ("t_kernel_ms", c_double),
         ("nonmonotone", c_uint32),
         ("jit_launches", c_uint32),
+        ("engines", c_uint32),
+        ("devices", c_uint32),
+        ("units_moved", c_uint64),
+        ("t_device_init_ms", c_double),
     ]
 
 
@@ -132,6 +136,8 @@ SIGNATURES = {
     "qi_search_shape": (c_int, [c_void_p, POINTER(Shape)]),
     "qi_fbas_jit_precompile": (c_int, [c_void_p, POINTER(c_double)]),
     "qi_search_wait_jit": (c_int, [c_void_p]),
+    "qi_hash_iteration_order": (c_int, [POINTER(c_uint32), c_uint32, POINTER(c_uint32), c_uint32, POINTER(c_uint32),
+                                        POINTER(c_uint32)]),
 }
 
 _lib = None
@@ -143,12 +149,21 @@ def lib() -> ctypes.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950) first")
+        # PyTorch-ROCm ships its own libamdhip64.so.7 (ROCm 7.0) with the same soname as
+        # /opt/rocm's (7.2): whichever loads first serves the whole process, and torch
+        # then refuses a runtime that is not its own ("No HIP GPUs are available").  Load
+        # torch's first, so the kernels and torch tensors/RCCL (multi-rank hand-offs)
+        # share one HIP runtime.  Without torch the system runtime is used.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.qi_abi_version() != 2:
+        if L.qi_abi_version() != 3:
             raise ImportError("libqi_amd.so ABI version mismatch")
         _lib = L
     return _lib

@@ -483,6 +483,15 @@ int qi_fbas_jit_precompile(qi_fbas* f, double* ms) {
   });
 }
 
+int qi_hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint32_t* seq, uint32_t n_seq,
+                            uint32_t* out, uint32_t* n_out) {
+  if ((n_keys && !keys) || (n_seq && !seq) || !out || !n_out) return fail(QI_ERR_ARG, "null argument");
+  return guarded([&] {
+    *n_out = qi::hash_iteration_order(keys, n_keys, seq, n_seq, out);
+    return QI_OK;
+  });
+}
+
 int qi_search_shape(const qi_search* s, qi_shape* out) {
   if (!s || !out) return fail(QI_ERR_ARG, "null");
   const qi::LocalFlat& L = s->lf;

@@ -112,6 +112,10 @@ class SearchDevice {
 };
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg);
 
+// The ordered kernel's libstdc++ unordered_set order emulation, on the host (tests).
+uint32_t hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint32_t* seq, uint32_t n_seq,
+                              uint32_t* out);
+
 // hipRTC-compile the specialised kernel for this SCC's template shape (no GPU needed).
 bool jit_precompile(const LocalFlat& f, std::string* log);
 

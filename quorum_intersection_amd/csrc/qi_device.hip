@@ -21,6 +21,7 @@
 //                  under early exit).
 // =====================================================================================
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <mutex>
@@ -49,6 +50,7 @@ namespace qi {
 }  // namespace qi
 
 #include "qi_search_kernel.h"
+#include "qi_ordered_kernel.h"
 
 namespace qi {
 namespace dev {
@@ -57,6 +59,12 @@ namespace dev {
 template <int MW, int TW, int SMAX>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
   search_body<MW, TW, SMAX, TableEval<MW, TW>>(a);
+}
+
+// Order-exact search for SCCs with threshold-0 quorum sets (qi_ordered_kernel.h).
+template <int MW, int TW>
+__global__ __launch_bounds__(64) void ordered_kernel(OrdArgs oa) {
+  ordered_body<MW, TW>(oa);
 }
 
 // Fold a host-known best witness into the device-side one (1-word keys).
@@ -68,15 +76,34 @@ __global__ void min_best_kernel(unsigned long long* best64, unsigned long long v
 // offset: out[q] = in[q * stride + (offset - q) mod stride].  (A plain stride keeps any
 // period of the frontier order that divides it: spilled stacks alternate size classes, and
 // stride 8 once gave ranks 10 M vs 19 M nodes.)
-template <int MW>
+template <int WORDS>
 __global__ void gather_units_kernel(const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt, uint32_t* out) {
-  using UL = UnitLayout<MW>;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t src = i * stride + (offset + stride - i % stride) % stride;
-    const uint4* s4 = (const uint4*)(in + src * UL::WORDS);
-    uint4* d4 = (uint4*)(out + i * UL::WORDS);
+    const uint4* s4 = (const uint4*)(in + src * WORDS);
+    uint4* d4 = (uint4*)(out + i * WORDS);
 #pragma unroll
-    for (int q = 0; q < UL::WORDS / 4; ++q) d4[q] = s4[q];
+    for (int q = 0; q < WORDS / 4; ++q) d4[q] = s4[q];
+  }
+}
+
+// frontier sort helpers (SearchDeviceImpl::sort_frontier)
+__global__ void iota_kernel(uint32_t* p, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = (uint32_t)i;
+}
+__global__ void unit_word_kernel(const uint32_t* units, uint32_t words, uint32_t off, const uint32_t* perm, uint64_t n,
+                                 uint32_t* keys) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    keys[i] = units[(uint64_t)perm[i] * words + off];
+}
+template <int WORDS>
+__global__ void gather_perm_kernel(const uint32_t* in, const uint32_t* perm, uint64_t n, uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4* s4 = (const uint4*)(in + (uint64_t)perm[i] * WORDS);
+    uint4* d4 = (uint4*)(out + i * WORDS);
+#pragma unroll
+    for (int q = 0; q < WORDS / 4; ++q) d4[q] = s4[q];
   }
 }
 
@@ -389,9 +416,11 @@ class GfpDeviceImpl : public GfpDevice {
   double last_ms_ = 0;
 };
 
-template <int MW, int TW, int SMAX>
+// ORD = false: search_kernel / the run-time specialised kernel (monotone SCCs);
+// ORD = true: ordered_kernel (SCCs with threshold-0 quorum sets), same protocol.
+template <int MW, int TW, int SMAX, bool ORD = false>
 class SearchDeviceImpl : public SearchDevice {
-  using UL = dev::UnitLayout<MW>;
+  using UL = std::conditional_t<ORD, dev::OrdUnitLayout<MW>, dev::UnitLayout<MW>>;
   using RL = dev::RecLayout<MW>;
   using WL = dev::WitLayout<MW>;
 
@@ -416,6 +445,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_COOP_BATCH")) cfg_.coop_batch = (uint32_t)std::atoi(e);
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
+    if (ORD) cfg_.jit = 1;  // no run-time specialisation of the ordered kernel
     stream_ = acquire_stream(device_);
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
@@ -464,6 +494,17 @@ class SearchDeviceImpl : public SearchDevice {
     for (uint32_t w = 0; w < 8; ++w) scc_mask_[w] = 0;
     for (uint32_t v = 0; v < f.m; ++v) scc_mask_[v >> 5] |= 1u << (v & 31);
     for (uint32_t w = 0; w < 8; ++w) d_.scc_mask[w] = scc_mask_[w];
+    if (ORD) {  // per-vertex roots, SCC-local adjacency, hash buckets of the global ids
+      keep(ord_.vroot = dupload(f.vroot, stream_));
+      keep(ord_.adj_off = dupload(f.ladj_off, stream_));
+      keep(ord_.adj = dupload(f.ladj, stream_));
+      std::vector<uint16_t> bm((size_t)5 * f.m);
+      for (uint32_t r = 0; r < 5; ++r)
+        for (uint32_t v = 0; v < f.m; ++v) bm[(size_t)r * f.m + v] = (uint16_t)(f.scc[v] % dev::kHashBuckets[r]);
+      keep(ord_.bktmod = dupload(bm, stream_));
+      ord_.smax = kOrdSmax;
+      ord_.depth_max = 32u * MW;
+    }
 
     cus_ = (uint32_t)device_cu_count(device_);
     max_blocks_ = cfg_.max_blocks ? cfg_.max_blocks : cus_ * 8u;  // refined below once shm_ is known
@@ -487,19 +528,23 @@ class SearchDeviceImpl : public SearchDevice {
     unsigned long long inf = ~0ull;
     HIP_CHECK(hipMemcpyAsync(best64_, &inf, 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
-    shm_ = (size_t)dev::search_lds_words<MW, SMAX>() * 4;
+    shm_ = ORD ? 0 : (size_t)dev::search_lds_words<MW, SMAX>() * 4;
     shm_ = (shm_ + 15) / 16 * 16;
     jit_shm_ = shm_ + (size_t)(jit_smax_ - SMAX) * (2 * MW + 1) * 64 * 4;  // QI_JIT_SMAX (diagnostics)
     if (jit_gstack()) jit_shm_ = (size_t)dev::search_lds_words<MW, SMAX, true>() * 4;
     jit_shm_ = (jit_shm_ + 15) / 16 * 16;
-    HIP_CHECK(hipFuncSetAttribute((const void*)dev::search_kernel<MW, TW, SMAX>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
+    const void* kfn;
+    if constexpr (ORD) kfn = (const void*)dev::ordered_kernel<MW, TW>;
+    else kfn = (const void*)dev::search_kernel<MW, TW, SMAX>;
+    if (!ORD) HIP_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
     if (!cfg_.max_blocks) {  // one resident wave of blocks: no second-wave tail
       int nb = 0;
-      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)dev::search_kernel<MW, TW, SMAX>, 64,
-                                                             shm_));
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 64, shm_));
+      if (ORD) nb = std::min(nb, 8);  // scratch-heavy lanes: a few waves per CU hide the latency
       if (nb > 0) max_blocks_ = cus_ * (uint32_t)nb;
     }
+    if (ORD)  // one DFS stack per lane of every block of a launch
+      keep(ord_.ostack = dalloc<uint32_t>((size_t)max_blocks_ * kOrdSmax * (dev::OrdUnitLayout<MW>::OWT + 2) * 64));
     lap("occupancy");
     if ((cfg_.jit == 2 || cfg_.jit == 3) && jit_eligible(flat_)) {
       start_jit();
@@ -526,6 +571,8 @@ class SearchDeviceImpl : public SearchDevice {
     (void)hipFree(red_);
     (void)hipFree(keydev_);
     (void)hipFree(wit_);
+    for (auto* p : {sk_[0], sk_[1], sp_[0], sp_[1]}) (void)hipFree(p);
+    (void)hipFree(stemp_);
     (void)hipEventDestroy(e0_);
     (void)hipEventDestroy(e1_);
     release_stream(device_, stream_);
@@ -538,7 +585,12 @@ class SearchDeviceImpl : public SearchDevice {
     DeviceGuard dg(device_);
     ensure_cap(0, 1);
     std::vector<uint32_t> u(UL::WORDS, 0);
-    for (int w = 0; w < MW; ++w) u[UL::T_ + w] = scc_mask_[w];  // toRemove = scc, dontRemove = {} (cpp:393)
+    if constexpr (ORD) {  // toRemove = scc in ascending order, dontRemove = {} (cpp:393)
+      u[UL::TLEN] = m_;
+      for (uint32_t v = 0; v < m_; ++v) u[UL::TORD + v / 4] |= v << (8 * (v % 4));
+    } else {
+      for (int w = 0; w < MW; ++w) u[UL::T_ + w] = scc_mask_[w];  // toRemove = scc, dontRemove = {} (cpp:393)
+    }
     HIP_CHECK(hipMemcpyAsync(units_[cur_], u.data(), UL::BYTES, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
     n_ = 1;
@@ -567,7 +619,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (cfg_.jit == 0 && launches_ >= cfg_.jit_after && jit_state_.load() == 0 && jit_eligible(flat_)) start_jit();
     if (jit_state_.load() == 2) load_jit();
     const bool spec = jit_fn_ != nullptr;
-    const uint32_t smax = spec ? (uint32_t)jit_smax_ : (uint32_t)SMAX;
+    const uint32_t smax = ORD ? kOrdSmax : (spec ? (uint32_t)jit_smax_ : (uint32_t)SMAX);
     const uint32_t blocks = max_blocks_;
     const uint32_t K = std::max(1u, std::min(cfg_.batch ? cfg_.batch : (uint32_t)kMaxBatch, (uint32_t)kMaxBatch));
     // growing to a target: no look-ahead, so the chain stops at the first launch past it
@@ -578,7 +630,7 @@ class SearchDeviceImpl : public SearchDevice {
     };
     auto first_need = [&](uint64_t n) {
       const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
-      return n + nb * 64u * (smax + 3 + cfg_.evict_max);  // search_body's need_out
+      return n + nb * 64u * (dev::spill_reserve(smax) + cfg_.evict_max);  // search_body's need_out
     };
     {
       const uint64_t need = first_need(n_);
@@ -639,7 +691,11 @@ class SearchDeviceImpl : public SearchDevice {
       a.prev = ctr_ + (size_t)k * dev::CTR_WORDS;
       a.counters = ctr_ + (size_t)(k + 1) * dev::CTR_WORDS;
       a.host_ctr = hctr_dev_ + (size_t)k * dev::HC_WORDS;
-      if (spec) {
+      if constexpr (ORD) {
+        dev::OrdArgs oa = ord_;
+        oa.a = a;
+        hipLaunchKernelGGL((dev::ordered_kernel<MW, TW>), dim3(blocks), dim3(64), 0, stream_, oa);
+      } else if (spec) {
         void* args[] = {&a};
         HIP_CHECK(hipModuleLaunchKernel(jit_fn_, blocks, 1, 1, 64, 1, 1, (unsigned)jit_shm_, stream_, args, nullptr));
       } else {
@@ -664,11 +720,15 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t g_wit = glob_host_[0], g_flags = glob_host_[1];
     if (g_flags & dev::FLAG_OUT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "search frontier buffer overflow");
     if (g_flags & dev::FLAG_WIT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "witness buffer overflow");
+    if (g_flags & dev::FLAG_DEPTH)  // zero-fallback steps that keep T (cpp:221, 343): the
+      // reference's recursion would not terminate either
+      throw Error(QI_ERR_STATE, "search path deeper than the path key (non-terminating recursion)");
     // walk the chain: launches that ran, the first stopped one, the final frontier
     uint32_t ran = 0, k = 0;
     bool stopped = false;
     double ms_sum = 0;
     uint64_t n_next = n_, log_next = lc.used;
+    bool halted = false;
     int cur_next = cur_;
     for (uint32_t j = 0; j < enq; ++j) {
       float ms = 0;
@@ -685,6 +745,7 @@ class SearchDeviceImpl : public SearchDevice {
       }
       cur_next = (cur_ + k + 1) & 1;
       n_next = c[dev::HC_OUT];
+      halted = c[dev::HC_HALT] != 0;
       log_next = c[dev::HC_LOGN];
       if (c[dev::HC_NIN] == 0) continue;
       ++ran;
@@ -709,6 +770,25 @@ class SearchDeviceImpl : public SearchDevice {
       if (lc.cap - lc.used < log_need(n_)) new_log_chunk(2 * log_need(n_));
       ++stops_;
     }
+    if (g_flags & dev::FLAG_POOL) {  // some lane found the eviction pool dry and stopped early:
+      // double the frontier buffers (the current frontier is preserved), so the next
+      // launches can dig deeper
+      const uint64_t c2 = 2 * std::min(cap_[0], cap_[1]);
+      ensure_cap(cur_, c2, true);
+      ensure_cap(1 - cur_, c2);
+      const uint32_t zero = 0;
+      HIP_CHECK(hipMemcpyAsync(glob_ + 1, &zero, 4, hipMemcpyHostToDevice, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      ++pool_growths_;
+    }
+    // The last launch that ran had to carry units over: its lanes spent their node budgets
+    // with units left, so launches no longer cover the frontier.  Serve it in preorder
+    // from now on: the preorder-first units (the only ones that can hold the first
+    // witness) go to lanes first, and nothing after a found witness starves it.
+    if (halted && n_ > 1) {
+      sort_frontier();
+      ++sorts_;
+    }
     // collect new witnesses (the buffer restarts at 0 for the next step)
     if (g_wit > 0) {
       const uint32_t nw = std::min(g_wit, wit_cap_);
@@ -720,8 +800,20 @@ class SearchDeviceImpl : public SearchDevice {
       si.new_witnesses = nw;
     }
     if (trace_)
-      std::fprintf(stderr, "[qi]   step: %u launches enqueued, %u ran, frontier %llu, %s, kernel %.3f ms\n", enq, ran,
-                   (unsigned long long)n_, stopped ? "capacity stop" : "chain end", si.dispatch_ms);
+      std::fprintf(stderr,
+                   "[qi]   step: %u launches enqueued, %u ran, processed %llu, frontier %llu, %s%s%s, wit %u, best %d, "
+                   "cap %llu, kernel %.3f ms\n",
+                   enq, ran, (unsigned long long)si.processed, (unsigned long long)n_,
+                   stopped ? (halted ? "halt+sort" : "capacity stop") : "chain end", (g_flags & dev::FLAG_POOL) ? ", pool dry" : "",
+                   "", g_wit, (int)has_best_, (unsigned long long)std::min(cap_[0], cap_[1]), si.dispatch_ms);
+    // no-progress guard: a step that ran no unit and did not shrink the frontier (its first
+    // launch stopped for capacity, which the host just fixed) may happen once in a row;
+    // more means the chain cannot advance, and the caller gets an error instead of a spin
+    if (si.processed == 0 && n_ >= si.frontier_in) {
+      if (++idle_steps_ > 4) throw Error(QI_ERR_STATE, "search step made no progress (frontier " + std::to_string(n_) + ")");
+    } else {
+      idle_steps_ = 0;
+    }
     si.frontier_out = n_;
     si.budget = cfg_.run_budget;
     si.blocks = blocks;
@@ -777,7 +869,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (cnt) {
       ensure_cap(1 - cur_, cnt);
       const uint32_t nb = (uint32_t)std::min<uint64_t>((cnt + 255) / 256, 4096);
-      hipLaunchKernelGGL(dev::gather_units_kernel<MW>, dim3(nb), dim3(256), 0, stream_, units_[cur_], offset, stride,
+      hipLaunchKernelGGL(dev::gather_units_kernel<UL::WORDS>, dim3(nb), dim3(256), 0, stream_, units_[cur_], offset, stride,
                          cnt, units_[1 - cur_]);
       HIP_CHECK(hipGetLastError());
       cur_ = 1 - cur_;
@@ -888,6 +980,51 @@ class SearchDeviceImpl : public SearchDevice {
 
   void keep(const void* p) { bufs_.push_back((void*)p); }
 
+  // Frontier into preorder: LSD radix passes (stable) over depth, then the path-key words
+  // from last to first, i.e. lexicographic (K[0], ..., K[MW-1], depth) = after_key order.
+  void sort_frontier() {
+    const uint64_t n = n_;
+    if (n > 0xFFFFFFFFull) throw Error(QI_ERR_CAPACITY, "frontier sort: too many units");
+    if (sort_cap_ < n) {
+      for (auto* p : {sk_[0], sk_[1], sp_[0], sp_[1]}) (void)hipFree(p);
+      (void)hipFree(stemp_);
+      sort_cap_ = std::max<uint64_t>(n, 1u << 16);
+      for (int i = 0; i < 2; ++i) {
+        sk_[i] = dalloc<uint32_t>(sort_cap_);
+        sp_[i] = dalloc<uint32_t>(sort_cap_);
+      }
+      stemp_bytes_ = 0;
+      HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, stemp_bytes_, sk_[0], sk_[1], sp_[0], sp_[1],
+                                                   (int)sort_cap_, 0, 32, stream_));
+      stemp_ = (void*)dalloc<uint8_t>(stemp_bytes_);
+    }
+    const uint32_t nb = (uint32_t)std::min<uint64_t>((n + 255) / 256, 65535);
+    hipLaunchKernelGGL(dev::iota_kernel, dim3(nb), dim3(256), 0, stream_, sp_[0], n);
+    for (int pass = 0; pass <= MW; ++pass) {  // pass 0: depth; pass p: K[MW - p]
+      const int off = pass == 0 ? UL::DEPTH : UL::K_ + MW - pass;
+      hipLaunchKernelGGL(dev::unit_word_kernel, dim3(nb), dim3(256), 0, stream_, units_[cur_], (uint32_t)UL::WORDS,
+                         (uint32_t)off, sp_[0], n, sk_[0]);
+      size_t tb = stemp_bytes_;
+      HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(stemp_, tb, sk_[0], sk_[1], sp_[0], sp_[1], (int)n, 0,
+                                                   pass == 0 ? 12 : 32, stream_));
+      std::swap(sp_[0], sp_[1]);
+    }
+    ensure_cap(1 - cur_, n);
+    hipLaunchKernelGGL(dev::gather_perm_kernel<UL::WORDS>, dim3(nb), dim3(256), 0, stream_, units_[cur_], sp_[0], n,
+                       units_[1 - cur_]);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    cur_ = 1 - cur_;
+  }
+  uint32_t* sk_[2] = {nullptr, nullptr};
+  uint32_t* sp_[2] = {nullptr, nullptr};
+  void* stemp_ = nullptr;
+  size_t stemp_bytes_ = 0;
+  uint64_t sort_cap_ = 0;
+  uint64_t sorts_ = 0;
+  static constexpr uint32_t kOrdSmax = 16;  // ordered kernel: stack levels per lane
+  dev::OrdArgs ord_{};
+
   void ensure_cap(int which, uint64_t units, bool preserve = false) {
     if (cap_[which] >= units) return;
     uint64_t nc = std::max<uint64_t>(units, cap_[which] * 2);
@@ -945,6 +1082,8 @@ class SearchDeviceImpl : public SearchDevice {
   uint64_t cap_[2] = {0, 0};
   int cur_ = 0;
   uint64_t n_ = 0;
+  uint32_t idle_steps_ = 0;    // consecutive steps without progress (guard)
+  uint64_t pool_growths_ = 0;  // buffer doublings after a dry eviction pool
   static constexpr uint32_t kMaxBatch = 64;
   uint32_t* ctr_ = nullptr;       // [kMaxBatch + 1][CTR_WORDS]: seed block + one per launch
   uint32_t* glob_ = nullptr;      // witness count, flags
@@ -1021,6 +1160,32 @@ class SearchDeviceImpl : public SearchDevice {
 
 }  // namespace
 
+// The ordered kernel's emulation of libstdc++ unordered_set iteration order, run on the
+// host (tests compare it with the real container): keys[v] = global index of local
+// vertex v; the table is built by inserting seq[0..n_seq) in order (repeats ignored).
+uint32_t hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint32_t* seq, uint32_t n_seq,
+                              uint32_t* out) {
+  if (n_keys > 256) throw Error(QI_ERR_ARG, "hash order: more than 256 keys");
+  auto* hl = new dev::HashList<256, 257>;
+  hl->clear();
+  std::vector<uint8_t> seen(n_keys, 0);
+  auto bmod = [&](uint32_t v, int r) -> uint32_t { return keys[v] % dev::kHashBuckets[r]; };
+  for (uint32_t i = 0; i < n_seq; ++i) {
+    const uint32_t v = seq[i];
+    if (v >= n_keys) {
+      delete hl;
+      throw Error(QI_ERR_ARG, "hash order: vertex out of range");
+    }
+    if (seen[v]) continue;
+    seen[v] = 1;
+    hl->insert((uint16_t)v, bmod);
+  }
+  uint32_t n = 0;
+  for (uint16_t v = hl->head; v != dev::HashList<256, 257>::NIL; v = hl->nxt[v]) out[n++] = v;
+  delete hl;
+  return n;
+}
+
 std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g) {
   return std::unique_ptr<GfpDevice>(new GfpDeviceImpl(device, g));
 }
@@ -1043,6 +1208,16 @@ bool jit_precompile(const LocalFlat& f, std::string* log) {
 
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg) {
   const uint32_t mw = f.mw, tw = f.tw;
+  // threshold-0 quorum sets: the order-exact kernel (QI_ORDERED=1 forces it, diagnostics)
+  const char* fo = std::getenv("QI_ORDERED");
+  if (f.nonmonotone || (fo && std::atoi(fo) != 0)) {
+    if (mw <= 1 && tw <= 1) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 1, 24, true>(device, f, cfg));
+    if (mw <= 1 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 4, 24, true>(device, f, cfg));
+    if (mw <= 2 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<2, 4, 16, true>(device, f, cfg));
+    if (mw <= 4 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<4, 8, 12, true>(device, f, cfg));
+    if (mw <= 8 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<8, 8, 8, true>(device, f, cfg));
+    throw Error(QI_ERR_UNSUPPORTED, "searched SCC too large for the device kernels (|SCC| > 256 or > 256 TNs)");
+  }
   if (mw <= 1 && tw <= 1) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 1, 24>(device, f, cfg));
   if (mw <= 1 && tw <= 2) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 2, 24>(device, f, cfg));
   if (mw <= 1 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 4, 24>(device, f, cfg));

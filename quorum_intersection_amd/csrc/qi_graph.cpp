@@ -459,6 +459,15 @@ LocalFlat flatten_local(const Graph& g, const std::vector<uint32_t>& scc) {
     L.root_users[(size_t)r * L.mw + (i >> 5)] |= 1u << (i & 31);
   }
   L.R = (uint32_t)L.root_tn.size();
+  L.vroot.assign(L.m, LocalFlat::NO_ROOT);
+  for (uint32_t i = 0; i < L.m; ++i)
+    if (live[root[i]]) L.vroot[i] = remap[root[i]];
+  L.ladj_off.assign(L.m + 1, 0);
+  for (uint32_t i = 0; i < L.m; ++i) {
+    for (uint32_t w : g.adj[scc[i]])
+      if (local[w] >= 0) L.ladj.push_back((uint32_t)local[w]);
+    L.ladj_off[i + 1] = (uint32_t)L.ladj.size();
+  }
 
   // findBestNode columns: in-edges from SCC members, with multiplicity (cpp:222-247)
   std::vector<std::vector<uint32_t>> col(L.m);

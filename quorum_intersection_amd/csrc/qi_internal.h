@@ -126,6 +126,13 @@ struct LocalFlat {
   // containsQuorum(X) is empty whenever |X| < qmin.  0 disables the test (threshold-0
   // sets make the slice predicate non-monotone).
   uint32_t qmin[2] = {0, 0};
+  // Order-exact search (threshold-0 SCCs, qi_ordered_kernel.h): the root TN of each
+  // vertex (NO_ROOT: never satisfied) and the out-edges inside the SCC in insertion
+  // order with repetitions (findBestNode's in-degrees, cpp:222-247).
+  static constexpr uint32_t NO_ROOT = 0xFFFFFFFFu;
+  std::vector<uint32_t> vroot;      // [m]
+  std::vector<uint32_t> ladj_off;   // [m+1]
+  std::vector<uint32_t> ladj;
 };
 LocalFlat flatten_local(const Graph& g, const std::vector<uint32_t>& scc);
 

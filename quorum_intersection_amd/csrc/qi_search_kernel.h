@@ -245,14 +245,25 @@ enum : int {
   C_HEAD = 1,      // dynamic claims past the statically assigned range           [atomic]
   C_DONE = 2,      // used blocks that finished                                   [atomic]
   C_XREC = 3,      // log records of stolen segments (after the n_in unit records) [atomic]
+  C_EVX = 4,       // stack evictions granted from the shared output pool          [atomic]
   C_NIN = 32,      // input units of this launch (the previous block's C_OUT)
   C_LOGB = 33,     // first segment-log record of this launch
   C_STOP = 34,     // 1: capacity would be exceeded; this launch (and the rest of the chain) did nothing
   C_STATIC = 35,   // end of the statically assigned range (64 units per used block)
   C_LOGN = 36,     // log base of the next launch (written by this launch's last block)
+  C_HALT = 37,     // 1: this launch carried units over (its lanes ran out of budget with
+                   // units left); the rest of the chain does nothing and the host sorts
+                   // the frontier into preorder before it goes on
   CTR_WORDS = 64,
-  HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_WORDS = 8
+  HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6, HC_WORDS = 8
 };
+// Output capacity per launch: n_in (carried-over units) + per used lane SPILL_RESERVE(S)
+// units for its one final spill (current node, top of stack, S stacked entries, a claimed
+// unit, one forced eviction) + a shared pool for stack evictions (>= evict_max per lane).
+// An eviction the pool cannot grant makes the lane spill and stop instead (FLAG_POOL); the
+// host then grows the buffers.  Every lane therefore digs as deep as its node budget
+// allows while there is room, and a launch never writes past out_cap.
+__host__ __device__ constexpr uint32_t spill_reserve(uint32_t smax) { return smax + 4u; }
 constexpr int TOT_SHARDS = 64;  // running totals: [TOT_SHARDS][16] u64, shard = block % 64
 
 struct SearchArgs {
@@ -288,7 +299,7 @@ struct SearchArgs {
   uint32_t* gstack;              // QI_GSTACK builds: [blocks][64 lanes][SMAX][2MW+1] DFS stacks
 };
 
-enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u };
+enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u, FLAG_POOL = 8u };
 
 // 64-bit preorder summary of a node (path key K, depth d) for the device-side best key:
 // MW == 1: (K0, d) -- exact order; MW > 1: (K0, K1) -- "strictly greater" still implies
@@ -435,7 +446,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // ---- chained launch prologue: input count, log position, capacity (wave-uniform) ----
   const uint32_t* pc = a.prev;
   uint32_t* cc = a.counters;
-  if (pc[C_STOP]) {  // an earlier launch of this chain stopped: the frontier stays where it is
+  if (pc[C_STOP] || pc[C_HALT]) {  // an earlier launch stopped or halted: the frontier stays
     if (blockIdx.x == 0 && lane == 0) {
       cc[C_STOP] = 1u;
       a.host_ctr[HC_STOP] = 1u;
@@ -447,10 +458,12 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   const uint32_t log_base = pc[C_LOGN];
   const uint32_t nb_used = min((n_in + (uint32_t)WAVE - 1u) / (uint32_t)WAVE, gridDim.x);
   const uint32_t static_end = min(n_in, nb_used * (uint32_t)WAVE);
+  // evictions share what the final spills and the carried-over units leave of out_cap
+  const uint64_t spill_need = (uint64_t)n_in + (uint64_t)nb_used * WAVE * spill_reserve(SMAX);
+  const uint32_t evict_pool = spill_need < (uint64_t)a.out_cap ? (uint32_t)((uint64_t)a.out_cap - spill_need) : 0u;
   {
-    // per lane at most: current node + top of stack + SMAX entries + a prefetched unit
-    // spilled once, plus evict_max evictions
-    const uint64_t need_out = (uint64_t)n_in + (uint64_t)nb_used * WAVE * (uint64_t)(SMAX + 3 + a.evict_max);
+    // the final spills, and at least evict_max evictions per used lane
+    const uint64_t need_out = spill_need + (uint64_t)nb_used * WAVE * (uint64_t)a.evict_max;
     const uint64_t need_log = (uint64_t)log_base + n_in + (uint64_t)nb_used * WAVE * (a.steal_max + 1u);
     const bool stop = need_out > (uint64_t)a.out_cap || need_log > (uint64_t)a.log_cap;
     if (blockIdx.x == 0 && lane == 0) {
@@ -501,7 +514,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     const uint32_t p = sbase_ + i;
     return p >= (uint32_t)SMAX ? p - (uint32_t)SMAX : p;
   };
-  uint32_t steps = 0, evictions = 0, steals = 0;
+  uint32_t steps = 0, steals = 0;
+  bool must_spill = false;  // an eviction found the pool empty: spill at the next iteration
   uint32_t xpool_next = 0, xpool_end = 0;  // wave-uniform: claimed extra log record slots
   uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
   bool dry = false;         // wave-uniform: no unit left to claim (head >= n_in)
@@ -931,7 +945,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     QI_STAMP(1);  // claims + polls
     // ---- (3) budget exhausted: spill current node, top, stack and claimed unit ---------
     {
-      const bool spill = (has && !park && (steps >= limit || evictions >= a.evict_max)) ||
+      const bool spill = (has && !park && (steps >= limit || must_spill)) ||
                          (!has && fpend && steps >= limit);
       if (__any(spill)) {
         uint32_t total = 0;
@@ -1028,14 +1042,25 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // exclusion branch (cpp:336): same D, T = T', key bit 0.
     {
       const bool evict = push && tvalid && nst == (uint32_t)SMAX;
+      bool forced = false;  // no pool slot: the old top leaves through this lane's spill reserve
       if (__any(evict)) {
+        const uint64_t em = __ballot(evict);
+        uint32_t tok = 0;
+        if (lane == 0) tok = atomicAdd(&cc[C_EVX], (uint32_t)__popcll(em));
+        tok = lane0(tok);
+        const bool granted = evict && tok + rank_in(em) < evict_pool;
+        forced = evict && !granted;
         uint32_t total = 0;
         const uint32_t slot = reserve<1>(evict ? 1u : 0u, &cc[C_OUT], total);
-        if (evict) {
+        if (granted) {
           write_lds_entry(slot, spos(0));
           sbase_ = spos(1);
           --nst;
-          ++evictions;
+        } else if (forced) {
+          write_entry(slot, tT, tD, tpk);
+          tvalid = false;
+          must_spill = true;
+          atomicOr(&a.glob[1], FLAG_POOL);
         }
       }
       if (push) {
@@ -1280,6 +1305,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (lane == 0) xr = atomicAdd(&cc[C_XREC], 0u);
       xr = lane0(xr);
       if (lane == 0) {
+        // never-claimed units: the global queue outlived every lane's node budget
+        cc[C_HALT] = left ? 1u : 0u;
+        a.host_ctr[HC_HALT] = left ? 1u : 0u;
         out += left;
         if (left) atomicExch(&cc[C_OUT], out);
         cc[C_LOGN] = log_base + n_in + xr;

@@ -177,3 +177,48 @@ def test_planted_deep_construction():
         a2 = [v in q2 for v in range(o.n)]
         assert all(o.slice(v, a2) for v in q2)
         assert all(o.slice(v, a1) for v in q1) == plant
+
+
+# ---- libstdc++ unordered_set order (toRemove, cpp:308/331) --------------------------------
+def _oracle_lib():
+    import ctypes
+    L = Oracle().L
+    L.qio_hash_order.restype = ctypes.c_uint64
+    L.qio_hash_order.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                 ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    L.qio_hash_bucket_counts.restype = None
+    L.qio_hash_bucket_counts.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
+    return L
+
+
+def test_hash_bucket_growth_is_the_emulated_one():
+    # the ordered search kernel assumes 13/29/59/127/257 buckets from the 1st/14th/30th/
+    # 60th/128th distinct insertion on (qi_ordered_kernel.h, hash_grow_at)
+    import ctypes
+    out = (ctypes.c_uint64 * 300)()
+    _oracle_lib().qio_hash_bucket_counts(300, out)
+    want = [13] * 13 + [29] * 16 + [59] * 30 + [127] * 68 + [257] * 130 + [541] * 43
+    assert list(out) == want
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_hash_iteration_order_matches_libstdcxx(seed):
+    # the product's emulation (host build of the device code) against the real container
+    import ctypes
+    import quorum_intersection_amd as qa
+    L, P = _oracle_lib(), qa.lib()
+    rng = random.Random(seed)
+    for trial in range(60):
+        n = rng.choice([1, 2, 5, 13, 14, 15, 29, 30, 31, 59, 60, 61, 127, 128, 129, 200, 256])
+        keys = rng.sample(range(rng.choice([n, 2 * n + 7, 600, 100000])), n)
+        seq = [rng.randrange(n) for _ in range(rng.randint(0, 2 * n))]
+        if rng.random() < 0.5:
+            seq = rng.sample(range(n), rng.randint(0, n))
+        K = (ctypes.c_uint32 * n)(*keys)
+        S = (ctypes.c_uint32 * max(len(seq), 1))(*seq)
+        want = (ctypes.c_uint32 * n)()
+        got = (ctypes.c_uint32 * n)()
+        nw = L.qio_hash_order(K, n, S, len(seq), want)
+        ng = ctypes.c_uint32()
+        qa.check(P.qi_hash_iteration_order(K, n, S, len(seq), got, ctypes.byref(ng)))
+        assert list(got)[: ng.value] == list(want)[:nw], (n, keys, seq)
