@@ -288,9 +288,12 @@ def main():
     if golden is None:
         line["golden"] = "no fixture for this workload"
     else:
-        ok = golden["nodes"] == res.nodes and bool(golden["verdict"]) == bool(res.verdict)
-        line["golden"] = "match (nodes, verdict)" if ok else (
-            f"MISMATCH: nodes {res.nodes} vs {golden['nodes']}, verdict {res.verdict} vs {golden['verdict']}")
+        # the metric's numerator (credited evals) is checked too, and minq / the witness
+        want = (golden["nodes"], golden["evals"], golden["minq"], bool(golden["verdict"]))
+        got = (res.nodes, evals_per_step, res.minq, bool(res.verdict))
+        ok = want == got and (res.verdict or (res.q1, res.q2) == (golden["q1"], golden["q2"]))
+        line["golden"] = "match (nodes, evals, minq, verdict, witness)" if ok else (
+            f"MISMATCH: (nodes, evals, minq, verdict) {got} vs {want}")
 
     if not args.no_cpu_baseline and world == 1:
         # median of 3 runs of the -O3 oracle, plus the -O0 build of the same

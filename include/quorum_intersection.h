@@ -46,6 +46,10 @@ const char* qi_last_error(void);
 int qi_abi_version(void);
 /* Number of visible HIP devices (0 when none). */
 int qi_device_count(void);
+/* Create the HIP context of `device` now (runtime + device initialisation, which the
+ * first device call would otherwise pay); *ms = wall time.  Lets a caller report device
+ * init apart from time-to-verdict. */
+int qi_device_warmup(int device, double* ms);
 
 /* ---------------------------------------------------------------------------------
  * FBAS: parseStellarConfigurationJSON + buildDependencyGraph + strong_components
@@ -135,6 +139,8 @@ int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32
  * (cpp:709-716) + verdict line (cpp:790-797).  Returns malloc'd text (free with
  * qi_free); *verdict = 1/0.  verbose/graphviz as -v/-g. */
 int qi_solve_text(qi_fbas* f, int verbose, int graphviz, char** text, int* verdict);
+/* The same with search options (engines, device_mask, budgets); opts may be NULL. */
+int qi_solve_text_ex(qi_fbas* f, int verbose, int graphviz, const qi_solve_opts* opts, char** text, int* verdict);
 /* computePageRank (cpp:718-733) text ("PageRank:" + "label: value" lines), host float. */
 int qi_pagerank_text(qi_fbas* f, float dangling, float convergence, uint64_t max_iterations, char** text);
 void qi_free(void* p);

@@ -247,7 +247,8 @@ class JsonReader {
 };
 
 // property_tree::get<size_t>: stream extraction of the text, whole string must be used
-// (stream_translator), else ptree_bad_data.  libstdc++ num_get rejects '-' for unsigned.
+// (stream_translator), else ptree_bad_data.  libstdc++ num_get accepts '-' for unsigned
+// and wraps ("-1" -> SIZE_MAX, no failbit).
 static size_t get_size_t(const PTree& t, const char* key) {
   const PTree* c = t.child(key);
   if (!c) throw ParseError(std::string("No such node (") + key + ")");

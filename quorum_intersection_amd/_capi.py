@@ -100,6 +100,7 @@ SIGNATURES = {
     "qi_last_error": (c_char_p, []),
     "qi_abi_version": (c_int, []),
     "qi_device_count": (c_int, []),
+    "qi_device_warmup": (c_int, [c_int, POINTER(c_double)]),
     "qi_fbas_from_json": (c_int, [c_char_p, c_size_t, c_int, POINTER(c_void_p)]),
     "qi_fbas_destroy": (None, [c_void_p]),
     "qi_fbas_num_vertices": (c_uint32, [c_void_p]),
@@ -111,6 +112,7 @@ SIGNATURES = {
     "qi_gfp_batch": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_uint32, POINTER(c_uint64)]),
     "qi_solve": (c_int, [c_void_p, POINTER(SolveOpts), POINTER(SolveResult), POINTER(c_uint32), POINTER(c_uint32)]),
     "qi_solve_text": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int)]),
+    "qi_solve_text_ex": (c_int, [c_void_p, c_int, c_int, POINTER(SolveOpts), POINTER(c_void_p), POINTER(c_int)]),
     "qi_pagerank_text": (c_int, [c_void_p, c_float, c_float, c_uint64, POINTER(c_void_p)]),
     "qi_free": (None, [c_void_p]),
     "qi_search_create": (c_int, [c_void_p, POINTER(SearchOpts), POINTER(c_void_p)]),

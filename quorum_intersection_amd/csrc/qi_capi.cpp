@@ -12,6 +12,7 @@
 
 #include "../../include/quorum_intersection.h"
 #include "qi_device.h"
+#include "qi_driver.h"
 #include "qi_internal.h"
 
 namespace {
@@ -107,47 +108,28 @@ qi::SearchConfig make_cfg(uint32_t grow, uint32_t run, uint32_t blocks, uint32_t
   return c;
 }
 
-struct SearchOutcome {
-  bool found = false;
-  bool nonmonotone = false;
-  qi::Totals totals;
-  std::vector<uint32_t> q1, q2;  // global indices
-  uint64_t launches = 0;
-  uint64_t jit_launches = 0;
-  double kernel_ms = 0;
-};
+// Engines of a search from the options: device_mask bits (0 = the FBAS's device), one
+// engine per device unless `engines` says otherwise (round-robin over the devices).
+std::vector<int> engine_devices(const qi_fbas* f, const qi_solve_opts* opts) {
+  std::vector<int> devs;
+  const uint32_t mask = opts ? opts->device_mask : 0u;
+  for (int d = 0; d < 32; ++d)
+    if ((mask >> d) & 1u) devs.push_back(d);
+  if (devs.empty()) devs.push_back(f->device);
+  const uint32_t E = (opts && opts->engines) ? opts->engines : (uint32_t)devs.size();
+  if (E > 64) throw qi::Error(QI_ERR_ARG, "at most 64 search engines");
+  std::vector<int> out;
+  for (uint32_t e = 0; e < E; ++e) out.push_back(devs[e % devs.size()]);
+  return out;
+}
 
-SearchOutcome run_search(qi_fbas* f, const qi::SearchConfig& cfg) {
-  if (qi::device_count() <= f->device || f->device < 0)
-    throw qi::Error(QI_ERR_DEVICE, "no HIP device for the search (the MI355X path has no CPU fallback)");
+qi::SearchOutcome run_search(qi_fbas* f, const qi::SearchConfig& cfg, const qi_solve_opts* opts) {
   const auto& scc = f->sccs.members.front();
-  const bool trace = std::getenv("QI_TRACE") != nullptr;  // diagnostics: host-side phase times
-  auto t0 = std::chrono::steady_clock::now();
-  qi::LocalFlat lf = qi::flatten_local(f->g, scc);
-  auto t1 = std::chrono::steady_clock::now();
-  auto sd = qi::make_search_device(f->device, lf, cfg);
-  auto t2 = std::chrono::steady_clock::now();
-  int steps = 0;
-  while (sd->frontier_size()) {
-    sd->step(0);
-    ++steps;
-  }
-  if (trace)
-    std::fprintf(stderr, "[qi] flatten %.3f ms, create %.3f ms, %d steps %.3f ms\n", ms_since(t0) - ms_since(t1),
-                 ms_since(t1) - ms_since(t2), steps, ms_since(t2));
-  SearchOutcome o;
-  o.nonmonotone = lf.nonmonotone;
-  qi::Witness w;
-  o.found = sd->best(&w);
-  o.totals = o.found ? sd->reduce(true, w.key, w.depth) : sd->running_totals();
-  if (o.found) {
-    for (uint32_t v : w.q1_local) o.q1.push_back(scc[v]);
-    for (uint32_t v : w.q2_local) o.q2.push_back(scc[v]);
-  }
-  o.launches = sd->launches();
-  o.jit_launches = sd->specialized_launches();
-  o.kernel_ms = sd->sum_kernel_ms();
-  return o;
+  const std::vector<int> ed = engine_devices(f, opts);
+  if (ed.size() == 1) return qi::search_front_scc(f->g, scc, ed[0], cfg);
+  qi::ShardConfig sc;
+  sc.engine_devices = ed;
+  return qi::search_front_scc_sharded(f->g, scc, sc, cfg);
 }
 
 }  // namespace
@@ -157,6 +139,16 @@ extern "C" {
 const char* qi_last_error(void) { return g_err.c_str(); }
 int qi_abi_version(void) { return QI_ABI_VERSION; }
 int qi_device_count(void) { return qi::device_count(); }
+
+int qi_device_warmup(int device, double* ms) {
+  return guarded([&] {
+    auto t0 = std::chrono::steady_clock::now();
+    if (qi::device_count() <= device || device < 0) throw qi::Error(QI_ERR_DEVICE, "no HIP device " + std::to_string(device));
+    qi::device_free(device, qi::device_alloc(device, 64));
+    if (ms) *ms = ms_since(t0);
+    return QI_OK;
+  });
+}
 
 int qi_fbas_from_json(const char* json, size_t len, int device, qi_fbas** out) {
   if (!json || !out) return fail(QI_ERR_ARG, "null argument");
@@ -230,11 +222,15 @@ int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32
     qi::SearchConfig cfg = make_cfg(opts ? opts->grow_budget : 0, opts ? opts->run_budget : 0,
                                     opts ? opts->max_blocks : 0, opts ? opts->jit : 0, opts ? opts->batch : 0);
     auto t1 = std::chrono::steady_clock::now();
-    SearchOutcome o = run_search(f, cfg);
+    qi::SearchOutcome o = run_search(f, cfg, opts);
     res->t_search_ms = ms_since(t1);
     res->t_kernel_ms = o.kernel_ms;
     res->launches = o.launches;
     res->jit_launches = (uint32_t)o.jit_launches;
+    res->engines = o.engines;
+    res->devices = o.devices;
+    res->units_moved = o.units_moved;
+    res->t_device_init_ms = o.t_device_init_ms;
     res->nodes = o.totals.nodes;
     res->evals += o.totals.evals;
     res->minq = o.totals.minq;
@@ -252,7 +248,12 @@ int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32
 
 // solve(istream&, ostream&, verbose, graphviz) text (cpp:615-716, 790-797)
 int qi_solve_text(qi_fbas* f, int verbose, int graphviz, char** text, int* verdict) {
+  return qi_solve_text_ex(f, verbose, graphviz, nullptr, text, verdict);
+}
+
+int qi_solve_text_ex(qi_fbas* f, int verbose, int graphviz, const qi_solve_opts* opts, char** text, int* verdict) {
   if (!f || !text || !verdict) return fail(QI_ERR_ARG, "null argument");
+  if (opts && opts->tiebreak != QI_TIE_LOWEST) return fail(QI_ERR_UNSUPPORTED, "only QI_TIE_LOWEST is implemented");
   return guarded([&] {
     std::ostringstream out;
     const auto& S = f->sccs.members;
@@ -279,7 +280,9 @@ int qi_solve_text(qi_fbas* f, int verbose, int graphviz, char** text, int* verdi
             << with.size() << "\n";
       result = false;
     } else {
-      SearchOutcome o = run_search(f, qi::SearchConfig());
+      qi::SearchConfig cfg = make_cfg(opts ? opts->grow_budget : 0, opts ? opts->run_budget : 0,
+                                      opts ? opts->max_blocks : 0, opts ? opts->jit : 0, opts ? opts->batch : 0);
+      qi::SearchOutcome o = run_search(f, cfg, opts);
       if (o.found) {
         if (verbose) {
           out << "found two non-intersecting quorums\n";

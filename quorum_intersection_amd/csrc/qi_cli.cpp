@@ -3,6 +3,16 @@
 // it (cpp:755-765): short and long forms, "-i 5" / "-i5" / "--max_iterations=5",
 // sticky short switches ("-vg"), unique long-option prefixes; anything else prints
 // "Invalid option!" and the option table and exits 1.
+//
+// Multi-GPU and diagnostics come from the environment, so the option table stays the
+// reference's:
+//   QI_DEVICES = all | 0,2,5 | 0-7   GPUs of the search (default: device 0); the search
+//                                    tree is sharded by branch prefix over them
+//   QI_ENGINES = N                   search shards (default: one per device; N > 1 on one
+//                                    device runs the same sharded path on one GPU)
+//   QI_TIMING  = 1                   one JSON line on stderr: device init, then stdin to
+//                                    verdict (parse + SCCs + checks + search) apart
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -137,6 +147,38 @@ bool parse_args(int argc, char** argv, Parsed& p) {
   return true;
 }
 
+// QI_DEVICES -> device mask; returns false on a malformed value
+bool parse_devices(const char* s, int ndev, uint32_t* mask) {
+  *mask = 0;
+  std::string v = s;
+  if (v == "all") {
+    for (int d = 0; d < ndev && d < 32; ++d) *mask |= 1u << d;
+    return *mask != 0;
+  }
+  size_t p = 0;
+  while (p < v.size()) {
+    size_t q = v.find(',', p);
+    if (q == std::string::npos) q = v.size();
+    const std::string item = v.substr(p, q - p);
+    const size_t dash = item.find('-');
+    uint64_t a = 0, b = 0;
+    if (dash == std::string::npos) {
+      if (!parse_u64(item, &a)) return false;
+      b = a;
+    } else if (!parse_u64(item.substr(0, dash), &a) || !parse_u64(item.substr(dash + 1), &b) || b < a) {
+      return false;
+    }
+    if (b >= 32) return false;
+    for (uint64_t d = a; d <= b; ++d) *mask |= 1u << d;
+    p = q + 1;
+  }
+  return *mask != 0;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 [[noreturn]] void die_parse(const char* what) {
   // the reference leaves the ptree_error uncaught: std::terminate -> SIGABRT
   std::cerr << "terminate called after throwing an instance of "
@@ -158,9 +200,36 @@ int main(int argc, char** argv) {
     std::cout << kHelp << std::endl;
     return EXIT_SUCCESS;
   }
+  const bool timing = std::getenv("QI_TIMING") != nullptr;
+  qi_solve_opts opts;
+  std::memset(&opts, 0, sizeof opts);
+  int device = 0;
+  if (const char* e = std::getenv("QI_DEVICES")) {
+    if (!parse_devices(e, qi_device_count(), &opts.device_mask)) {
+      std::cerr << "quorum_intersection: bad QI_DEVICES value '" << e << "'" << std::endl;
+      return 3;
+    }
+    while (!((opts.device_mask >> device) & 1u)) ++device;  // per-SCC checks on the first
+  }
+  if (const char* e = std::getenv("QI_ENGINES")) {
+    uint64_t n = 0;
+    if (!parse_u64(e, &n) || n == 0 || n > 64) {
+      std::cerr << "quorum_intersection: bad QI_ENGINES value '" << e << "'" << std::endl;
+      return 3;
+    }
+    opts.engines = (uint32_t)n;
+  }
+  double init_ms = 0;
+  if (timing && !p.pagerank) {  // HIP runtime + device context, reported apart
+    if (qi_device_warmup(device, &init_ms) != QI_OK) {
+      std::cerr << "quorum_intersection: " << qi_last_error() << std::endl;
+      return 3;
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();  // stdin open -> verdict printed
   std::string in((std::istreambuf_iterator<char>(std::cin)), std::istreambuf_iterator<char>());
   qi_fbas* f = nullptr;
-  int rc = qi_fbas_from_json(in.data(), in.size(), 0, &f);
+  int rc = qi_fbas_from_json(in.data(), in.size(), device, &f);
   if (rc == QI_ERR_PARSE) die_parse(qi_last_error());
   if (rc != QI_OK) {
     std::cerr << "quorum_intersection: " << qi_last_error() << std::endl;
@@ -179,13 +248,19 @@ int main(int argc, char** argv) {
     return EXIT_SUCCESS;
   }
   int verdict = 0;
-  rc = qi_solve_text(f, p.verbose ? 1 : 0, p.graph ? 1 : 0, &text, &verdict);
+  const double parse_ms = ms_since(t0);
+  rc = qi_solve_text_ex(f, p.verbose ? 1 : 0, p.graph ? 1 : 0, &opts, &text, &verdict);
   if (rc != QI_OK) {
     std::cerr << "quorum_intersection: " << qi_last_error() << std::endl;
     return 3;
   }
-  std::cout << text;
+  std::cout << text << std::flush;
   qi_free(text);
+  if (timing)
+    std::fprintf(stderr,
+                 "{\"device_init_ms\": %.3f, \"stdin_to_verdict_ms\": %.3f, \"parse_ms\": %.3f, "
+                 "\"devices_mask\": %u, \"engines\": %u}\n",
+                 init_ms, ms_since(t0), parse_ms, opts.device_mask, opts.engines);
   qi_fbas_destroy(f);
   return verdict ? EXIT_SUCCESS : EXIT_FAILURE;
 }

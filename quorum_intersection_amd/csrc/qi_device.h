@@ -81,6 +81,7 @@ struct Witness {
 class SearchDevice {
  public:
   virtual ~SearchDevice() = default;
+  virtual int device() const = 0;                   // HIP ordinal the engine runs on
   virtual uint32_t key_words() const = 0;
   virtual uint32_t unit_bytes() const = 0;
   virtual void reset_root() = 0;                    // frontier = {root of cpp:393}
@@ -121,5 +122,14 @@ bool jit_precompile(const LocalFlat& f, std::string* log);
 
 int device_count();
 int device_cu_count(int device);
+
+// Device memory for frontier hand-offs between engines (qi_shard.cpp): units move
+// device-to-device, across GPUs over xGMI with hipMemcpyPeerAsync.
+void* device_alloc(int device, size_t bytes);
+void device_free(int device, void* p);
+void device_copy(void* dst, int dst_device, const void* src, int src_device, size_t bytes);
+// Enable peer access from a to b (and b to a); false when the pair has no peer path
+// (copies then stage through the host inside the HIP runtime).
+bool enable_peer(int a, int b);
 
 }  // namespace qi

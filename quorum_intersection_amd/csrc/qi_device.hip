@@ -277,6 +277,56 @@ int device_cu_count(int device) {
   return p.multiProcessorCount;
 }
 
+void* device_alloc(int device, size_t bytes) {
+  int prev = 0;
+  HIP_CHECK(hipGetDevice(&prev));
+  HIP_CHECK(hipSetDevice(device));
+  void* p = nullptr;
+  const hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) throw Error(QI_ERR_CAPACITY, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return p;
+}
+
+void device_free(int device, void* p) {
+  if (!p) return;
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return;
+  (void)hipSetDevice(device);
+  (void)hipFree(p);
+  (void)hipSetDevice(prev);
+}
+
+void device_copy(void* dst, int dst_device, const void* src, int src_device, size_t bytes) {
+  if (!bytes) return;
+  int prev = 0;
+  HIP_CHECK(hipGetDevice(&prev));
+  HIP_CHECK(hipSetDevice(src_device));
+  if (dst_device == src_device) HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+  else HIP_CHECK(hipMemcpyPeer(dst, dst_device, src, src_device, bytes));  // xGMI
+  HIP_CHECK(hipSetDevice(prev));
+}
+
+bool enable_peer(int a, int b) {
+  if (a == b) return true;
+  int ab = 0, ba = 0;
+  if (hipDeviceCanAccessPeer(&ab, a, b) != hipSuccess || hipDeviceCanAccessPeer(&ba, b, a) != hipSuccess) return false;
+  if (!ab || !ba) return false;
+  int prev = 0;
+  HIP_CHECK(hipGetDevice(&prev));
+  for (auto pr : {std::make_pair(a, b), std::make_pair(b, a)}) {
+    HIP_CHECK(hipSetDevice(pr.first));
+    const hipError_t e = hipDeviceEnablePeerAccess(pr.second, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+      (void)hipSetDevice(prev);
+      return false;
+    }
+    (void)hipGetLastError();  // clear "already enabled"
+  }
+  HIP_CHECK(hipSetDevice(prev));
+  return true;
+}
+
 namespace {
 
 // hipStreamCreate costs ~2 ms on this stack (measured, QI_TRACE): engines take their stream
@@ -578,6 +628,7 @@ class SearchDeviceImpl : public SearchDevice {
     release_stream(device_, stream_);
   }
 
+  int device() const override { return device_; }
   uint32_t key_words() const override { return MW; }
   uint32_t unit_bytes() const override { return UL::BYTES; }
 

@@ -7,7 +7,8 @@
 //  * arrays are children with empty keys; objects keep duplicate keys, get() takes the
 //    first one; a top-level object is walked member by member like an array;
 //  * get<size_t>("threshold") parses the text with operator>> and requires that the
-//    whole text (up to trailing blanks) is consumed; '-' is rejected for unsigned;
+//    whole text (up to trailing blanks) is consumed; libstdc++ num_get accepts a leading
+//    '-' for unsigned and wraps ("-1" -> SIZE_MAX, no failbit), as property_tree does;
 //  * a quorum set with no children (null, {}, [], "x", 3) is an empty quorum set;
 //  * missing publicKey / quorumSet / threshold / validators / innerQuorumSets -> error.
 // Errors are reported as qi::Error(QI_ERR_PARSE); the reference aborts (uncaught ptree_error).

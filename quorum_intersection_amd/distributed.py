@@ -380,7 +380,9 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
                     w[0, 1:1 + len(a)] = torch.tensor(a, dtype=torch.int64, device=device)
                 if b:
                     w[1, 1:1 + len(b)] = torch.tensor(b, dtype=torch.int64, device=device)
-            dist.broadcast(w, owner, group=group)
+            # `owner` indexes the group's ranks; broadcast takes a global rank
+            src = dist.get_global_rank(group, owner) if group is not None else owner
+            dist.broadcast(w, src, group=group)
             wl = w.tolist()
             q1 = [int(x) for x in wl[0][1:1 + int(wl[0][0])]]
             q2 = [int(x) for x in wl[1][1:1 + int(wl[1][0])]]

@@ -312,6 +312,24 @@ def test_cli_binary_verdicts_and_exit_codes():
         assert r.stdout.decode() == Oracle().load(fixture_text(name)).solve_text(True, False)
 
 
+def test_cli_threshold_minus_one_matches_oracle():
+    # "threshold": "-1" wraps to SIZE_MAX (never satisfiable); the drop-in CLI and the
+    # oracle CLI agree byte for byte on the verdict and the -v text
+    import subprocess
+    nodes = [{"publicKey": k, "name": k.lower(), "quorumSet": {"threshold": 2, "validators": ["A", "B", "C"],
+                                                               "innerQuorumSets": []}} for k in "ABC"]
+    nodes.append({"publicKey": "D", "name": "d", "quorumSet": {"threshold": "-1", "validators": ["A", "D"],
+                                                             "innerQuorumSets": []}})
+    text = json.dumps(nodes).encode()
+    exe = os.path.join(ROOT, "bin", "quorum_intersection")
+    orc = os.path.join(ROOT, "oracle", "_build", "qi_oracle")
+    for flags in ([], ["-v"]):
+        a = subprocess.run([exe] + flags, input=text, capture_output=True)
+        b = subprocess.run([orc] + flags, input=text, capture_output=True)
+        assert (a.stdout, a.returncode) == (b.stdout, b.returncode), flags
+    assert a.returncode == 0  # A, B, C intersect; D never has a slice
+
+
 # ---- step-wise search with frontier hand-off (the multi-rank protocol on one GPU) -------
 def _two_way_search(text, hand_every=1, move_frac=0.5):
     import ctypes
@@ -519,3 +537,48 @@ def test_coop_batch_exact(name, batch, monkeypatch):
         assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"], r["evals"], r["minq"])
         if not r["verdict"]:
             assert d["q1"] == r["q1"] and d["q2"] == r["q2"]
+
+
+# ---- sharded search inside the library (qi_solve_opts.engines / device_mask) ---------------
+# The same code path as a multi-GPU solve: engine 0 grows, every engine keeps its dealt
+# share, engines run chains on their own host threads and streams, best keys and surplus
+# units move between chains.  On this one-GPU box all engines share device 0.
+@pytest.mark.parametrize("engines", [2, 3, 5])
+@pytest.mark.parametrize("name", ["tiered_5", "tiered_6", "broken", "planted_5_96", "tiered_5_shuffled", "random_28",
+                                  "two_tier_7_256"])
+def test_sharded_solve_exact(name, engines):
+    d = qa.FBAS(_text_for(name)).solve_stats(engines=engines, device_mask=1)
+    _cmp(d, GOLD[name], name)
+    if d["searched"]:
+        assert d["engines"] == engines and d["devices"] == 1
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 3))
+def test_sharded_random_threshold0_and_monotone(seed):
+    for t0 in (False, True):
+        text = random_org_fbas(seed, n_orgs=6 + seed % 3, t0=t0)
+        r = Oracle().load(text).solve()
+        d = qa.FBAS(text).solve_stats(engines=2 + seed % 3, grow_budget=1, run_budget=16)
+        _cmp(d, r, f"org{'_t0' if t0 else ''}{seed}")
+
+
+def test_sharded_bench_workloads_exact():
+    # configs[2] and configs[4] through 4 engines: full search and deep early exit
+    for name, text in (("two_tier_8_192", fbas_gen.two_tier(8, 192)), ("planted_deep_8_512", fbas_gen.planted_deep(8, 512))):
+        g = BIG[name]
+        d = qa.FBAS(text).solve_stats(engines=4, jit=2)
+        _cmp(d, g, name)
+
+
+def test_cli_sharded_engines_match_oracle(monkeypatch):
+    import subprocess
+    exe = os.path.join(ROOT, "bin", "quorum_intersection")
+    env = dict(os.environ, QI_DEVICES="0", QI_ENGINES="3", QI_TIMING="1")
+    for name in FIXTURES + ["tiered_5"]:
+        text = fixture_text(name) if name in FIXTURES else _text_for(name).encode()
+        r = subprocess.run([exe, "-v"], input=text, capture_output=True, env=env)
+        assert r.stdout.decode() == Oracle().load(text).solve_text(True, False), name
+        timing = json.loads(r.stderr.decode().strip().splitlines()[-1])
+        assert timing["engines"] == 3 and timing["stdin_to_verdict_ms"] > 0
+    r = subprocess.run([exe], input=fixture_text("correct"), capture_output=True, env=dict(os.environ, QI_DEVICES="0,31"))
+    assert r.returncode == 3 and b"no HIP device 31" in r.stderr  # a missing device fails loudly

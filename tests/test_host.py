@@ -75,6 +75,12 @@ EDGE_CASES = {
                                                                          "innerQuorumSets": []}}]),
     "threshold_negative": json.dumps([{"publicKey": "A", "quorumSet": {"threshold": -1, "validators": ["A"],
                                                                         "innerQuorumSets": []}}]),
+    # property_tree keeps "-1" as text and get<size_t> wraps it to SIZE_MAX (libstdc++
+    # num_get, no failbit): a never-satisfiable threshold, not a parse error
+    "threshold_negative_string": json.dumps([{"publicKey": "A", "quorumSet": {"threshold": "-1", "validators": ["A"],
+                                                                               "innerQuorumSets": []}}]),
+    "threshold_minus_zero": json.dumps([{"publicKey": "A", "quorumSet": {"threshold": "-0", "validators": ["A"],
+                                                                          "innerQuorumSets": []}}]),
     "threshold_float": json.dumps([{"publicKey": "A", "quorumSet": {"threshold": 1.0, "validators": ["A"],
                                                                      "innerQuorumSets": []}}]),
     "missing_validators": json.dumps([{"publicKey": "A", "quorumSet": {"threshold": 1, "innerQuorumSets": []}}]),
