@@ -32,6 +32,10 @@ sys.path.insert(0, ROOT)
 # VALU op issues in 2 cycles on a SIMD32 (MI355X_MICROARCH.md, chip table + "wave
 # scheduling"; the same rate gives its 157.3 TFLOP/s fp32 FMA peak).
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# Aggregate ds_read_b32 rate with every CU streaming (MI355X_MICROARCH.md, LDS section).
+LDS_PEAK_TBS = 75.0
+PEAKS_JSON = os.path.join(ROOT, "profiles", "r02", "peaks.json")        # tools/peak_probe.hip on the box
+CPU_FULL_JSON = os.path.join(ROOT, "profiles", "r02", "cpu_full.json")  # tools/cpu_full.py on the box host
 
 
 def ops_per_round(sh):
@@ -42,6 +46,15 @@ def ops_per_round(sh):
     w = sh["mask_words"]
     return (sh["tns"] * (2 * w + 2) + sh["tns_with_children"] * 2 + 2 * sh["extra_terms"]
             + sh["roots"] * (w + 2) + 2 * w)
+
+
+def lds_bytes_per_round(sh):
+    """SURVEY.md §8d's LDS side: the bytes a Jacobi round would read if the threshold-node
+    masks sat in LDS (4 B per 32-bit word per vertex word and per child word, extra planes
+    included).  The specialised kernel holds them as instruction literals / SGPRs instead,
+    so this is the model's demand, not traffic the kernel issues."""
+    w = sh["mask_words"]
+    return 4 * (sh["tns"] * w + sh["tns_with_children"] + sh["extra_terms"])
 
 
 def ops_per_best(sh):
@@ -150,13 +163,14 @@ def main():
     qa.FBAS(fbas_gen.tiered(2), device=gpu).solve_stats()
     device_init_s = time.perf_counter() - t0
 
-    # ---- time-to-verdict from JSON text (host parse + flatten + upload + solve), N=1 path
-    t0 = time.perf_counter()
     fb = qa.FBAS(text, device=gpu)
-    ttv_res = fb.solve_stats(args.grow_budget, args.run_budget, args.max_blocks)  # jit auto (CLI default)
-    time_to_verdict = time.perf_counter() - t0
-
     be = DeviceSearch(fb, args.grow_budget, args.run_budget, args.max_blocks, jit=args.jit, batch=batch)
+
+    # ---- time-to-verdict from JSON text (host parse + flatten + upload + solve), N=1 path,
+    # with the CLI's policy: the specialised kernel from the on-disk cache (filled above)
+    t0 = time.perf_counter()
+    ttv_res = qa.FBAS(text, device=gpu).solve_stats(args.grow_budget, args.run_budget, args.max_blocks, jit=4)
+    time_to_verdict = time.perf_counter() - t0
     shape = be.shape()
     sccs = fb.sccs()
     scc_masks = qa.masks_from_sets(sccs, fb.n)
@@ -213,6 +227,10 @@ def main():
     avg_launch_ms = dispatch_ms_all / max(dispatches_all, 1)
     alg_ops_launch = alg_ops_step * args.steps / max(dispatches_all, 1)
     achieved = alg_ops_launch / (avg_launch_ms * 1e-3) / 1e12 if avg_launch_ms > 0 else 0.0
+    lds_launch = res.rounds * lds_bytes_per_round(shape) * args.steps / max(dispatches_all, 1)
+    lds_achieved = lds_launch / (avg_launch_ms * 1e-3) / 1e12 if avg_launch_ms > 0 else 0.0
+    measured = json.load(open(PEAKS_JSON)) if os.path.exists(PEAKS_JSON) else {}
+    mix_peak = measured.get("valu_and_bcnt_pair_tops")
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -263,6 +281,15 @@ def main():
             "unit": "Tops/s (int32 lane-ops)",
             "frac": achieved / VALU_PEAK_TOPS,
             "traffic": traffic,
+            "frac_of_measured_mix_peak": (achieved / mix_peak) if mix_peak else None,
+            "measured_peaks": measured or None,
+            "peak_note": ("peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops (MI355X_MICROARCH.md); "
+                          "tools/peak_probe.hip on the box: v_and/v_add reach ~62 T, v_bcnt_u32_b32 is half rate "
+                          "(~35 T), the fixpoint's and+bcnt pair ~43 T (profiles/r02/peaks.json)"),
+            "lds_model": {"bytes_per_launch": lds_launch, "achieved": lds_achieved, "peak": LDS_PEAK_TBS,
+                          "unit": "TB/s", "frac": lds_achieved / LDS_PEAK_TBS,
+                          "note": "SURVEY §8d LDS-side model (TN masks per round); the kernel serves them from "
+                                  "instruction literals / SGPRs, so LDS is not the bound"},
             "kernel": "qi_search_spec (run-time specialised search_kernel)" if specialised else "search_kernel",
             "avg_launch_ms": avg_launch_ms,
             "launches_per_step": launches_all / args.steps / world,
@@ -274,7 +301,8 @@ def main():
         },
         "time_to_verdict_s": time_to_verdict,
         "time_to_verdict_note": ("N=1 path from JSON text in host memory: parse, SCCs, flatten, upload, solve "
-                                 "(CLI default: specialised kernel from the on-disk cache); device init apart"),
+                                 "(CLI policy jit=4: specialised kernel from the on-disk cache); device init apart; "
+                                 "the drop-in executable's stdin-to-verdict: tools/ttv_cli.sh"),
         "device_init_s": device_init_s,
     }
     if ttv_res["nodes"] != res.nodes or ttv_res["evals"] != evals_per_step:
@@ -323,6 +351,13 @@ def main():
             },
         }
         line["speedup_vs_cpu"] = value / cpu_evals_s
+        if os.path.exists(CPU_FULL_JSON):  # one complete CPU search of this workload, same host type
+            full = json.load(open(CPU_FULL_JSON))
+            if full.get("workload") == f"two_tier({args.k_top}, {args.validators})" and args.workload == "two_tier":
+                line["cpu_baseline"]["full_run"] = {k: full[k] for k in ("search_seconds", "evals_per_s", "nodes", "evals",
+                                                                         "host_cpu", "cores")}
+                line["cpu_baseline"]["full_run"]["source"] = "profiles/r02/cpu_full.json (tools/cpu_full.py)"
+                line["speedup_vs_cpu_full_run"] = full["search_seconds"] / (ms_per_step / 1e3)
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -87,9 +87,11 @@ typedef struct {
   uint32_t grow_budget;    /* 0 = default: per-lane node budget while the frontier grows */
   uint32_t run_budget;     /* 0 = default: per-lane node budget at full occupancy */
   uint32_t max_blocks;     /* 0 = default (8 wavefronts per CU) */
-  uint32_t jit;            /* run-time specialised search kernel: 0 auto (background compile
-                              once a search needs >= 3 launches), 1 off, 2 before launch 1,
-                              3 = 2 + diagnostic section stamps (not for measurement) */
+  uint32_t jit;            /* run-time specialised search kernel: 0 auto (from the on-disk
+                              cache if there, else compiled in the background once a search
+                              needs >= 3 launches), 1 off, 2 before launch 1, 3 = 2 +
+                              diagnostic section stamps (not for measurement), 4 cache only
+                              (never compiles; the CLI's choice) */
   uint32_t batch;          /* 0 = default: search launches chained on the device per host
                               synchronisation (each reads its input count from the previous) */
   uint32_t engines;        /* search shards: 0 = one per selected device.  Shards split the

@@ -480,6 +480,7 @@ int qi_fbas_jit_precompile(qi_fbas* f, double* ms) {
     auto t0 = std::chrono::steady_clock::now();
     qi::LocalFlat lf = qi::flatten_local(f->g, f->sccs.members.front());
     std::string log;
+    if (lf.nonmonotone) throw qi::Error(QI_ERR_UNSUPPORTED, "jit: threshold-0 SCCs run the ordered kernel");
     if (!qi::jit_precompile(lf, &log)) throw qi::Error(QI_ERR_UNSUPPORTED, "jit: " + log);
     if (ms) *ms = ms_since(t0);
     return QI_OK;

@@ -47,7 +47,9 @@ struct SearchConfig {
   // Run-time specialised kernel (qi_jit.cpp): 0 = auto (compile in the background once a
   // search reaches `jit_after` launches, switch at the next launch boundary), 1 = off
   // (table-interpreting kernel only), 2 = sync (compile before the first launch),
-  // 3 = sync diagnostic build with s_memtime section stamps (never for measurements).
+  // 3 = sync diagnostic build with s_memtime section stamps (never for measurements),
+  // 4 = cache only (the specialised kernel if the on-disk cache holds it, else the table
+  // kernel; never compiles).  0 and 4 load a cached kernel before the first launch.
   uint32_t jit = 0;
   uint32_t jit_after = 3;
 };

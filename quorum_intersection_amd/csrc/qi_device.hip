@@ -596,6 +596,16 @@ class SearchDeviceImpl : public SearchDevice {
     if (ORD)  // one DFS stack per lane of every block of a launch
       keep(ord_.ostack = dalloc<uint32_t>((size_t)max_blocks_ * kOrdSmax * (dev::OrdUnitLayout<MW>::OWT + 2) * 64));
     lap("occupancy");
+    if ((cfg_.jit == 0 || cfg_.jit == 4) && jit_eligible(flat_)) {
+      // auto / cache-only: a specialised kernel already in the on-disk cache runs from the
+      // first launch (hipModuleLoadData, ~1 ms); auto compiles a missing one in the
+      // background once the search proves long (step()), cache-only never compiles
+      jit_code_ = jit_cached(jit_source(flat_, MW, TW, jit_smax_, false, jit_gstack()));
+      if (!jit_code_.empty()) {
+        jit_state_.store(2);
+        load_jit();
+      }
+    }
     if ((cfg_.jit == 2 || cfg_.jit == 3) && jit_eligible(flat_)) {
       start_jit();
       if (!wait_jit()) throw Error(QI_ERR_UNSUPPORTED, "specialised kernel failed to build: " + jit_log_);

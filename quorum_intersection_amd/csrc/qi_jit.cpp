@@ -202,21 +202,28 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   return o.str();
 }
 
+std::string cache_path(const std::string& src) {
+  char key[32];
+  const char* xf = std::getenv("QI_JIT_FLAGS");
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v1|" + (xf ? xf : "")));
+  return cache_dir() + "/" + key + ".co";
+}
+
+std::vector<char> jit_cached(const std::string& src) {
+  std::ifstream in(cache_path(src), std::ios::binary);
+  if (!in) return {};
+  return std::vector<char>((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+}
+
 std::vector<char> jit_compile(const std::string& src, std::string* log) {
   if (const char* d = std::getenv("QI_JIT_DUMP")) {  // diagnostics: keep the generated source
     std::ofstream(d) << src;
   }
   const std::string dir = cache_dir();
-  char key[32];
-  const char* xf = std::getenv("QI_JIT_FLAGS");
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v1|" + (xf ? xf : "")));
-  const std::string path = dir + "/" + key + ".co";
+  const std::string path = cache_path(src);
   {
-    std::ifstream in(path, std::ios::binary);
-    if (in) {
-      std::vector<char> code((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-      if (!code.empty()) return code;
-    }
+    std::vector<char> code = jit_cached(src);
+    if (!code.empty()) return code;
   }
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "qi_search_spec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {

@@ -16,5 +16,7 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
 bool jit_gstack();
 // Compile for gfx950 (or read the on-disk cache); empty on failure, log in *log.
 std::vector<char> jit_compile(const std::string& src, std::string* log);
+// The code object from the on-disk cache only (no compile); empty when absent.
+std::vector<char> jit_cached(const std::string& src);
 
 }  // namespace qi
