@@ -37,6 +37,8 @@ struct SearchConfig {
   uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output; 8 stalls deep
                                  // multi-word searches, 8/32/64 equal on the bench)
   uint32_t run_at = 4;           // run budget once the frontier holds >= run_at/8 of the resident lanes
+  uint32_t mid_budget = 0;       // budget between run_at/8 and full_at/8 of the lanes (0 = run budget)
+  uint32_t full_at = 8;
   uint32_t steal_max = 0;        // per-lane entries taken from busy lanes per launch (bounds the log);
                                  // 0 = off: measured 4.6 vs 4.0 ms per search with 16 (QI_STEAL)
   uint32_t coop_batch = 1;       // parked quorum leaves per cooperative phase (QI_COOP_BATCH; 1 = every

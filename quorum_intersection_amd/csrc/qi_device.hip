@@ -492,6 +492,8 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_STEAL")) cfg_.steal_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_MID_BUDGET")) cfg_.mid_budget = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_FULL_AT")) cfg_.full_at = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_COOP_BATCH")) cfg_.coop_batch = (uint32_t)std::atoi(e);
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
@@ -723,6 +725,8 @@ class SearchDeviceImpl : public SearchDevice {
     a.grace = cfg_.grace;
     a.steal_max = cfg_.steal_max;
     a.run_at = cfg_.run_at;
+    a.mid_budget = cfg_.mid_budget;
+    a.full_at = cfg_.full_at;
     a.evict_max = cfg_.evict_max;
     a.half_m = m_ / 2;
     {  // cooperative slot: smallest power of two covering |D| + 1 <= half_m + 1 jobs

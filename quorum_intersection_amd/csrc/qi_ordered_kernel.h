@@ -285,7 +285,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     if (stop || blockIdx.x >= nb_used) return;
   }
   uint32_t* const records = a.records + (size_t)log_base * RL::WORDS;
-  const uint32_t budget = ((uint64_t)n_in * 8u >= (uint64_t)gridDim.x * WAVE * a.run_at) ? a.run_budget : a.grow_budget;
+  const uint32_t budget = launch_budget(a, n_in);
   uint32_t* const st = oa.ostack + (size_t)blockIdx.x * (oa.smax * SEW * WAVE);
 #define OST(lvl, w) st[((size_t)(lvl) * SEW + (w)) * WAVE + lane]
 

@@ -287,6 +287,8 @@ struct SearchArgs {
   uint32_t grace;                // extra steps per lane once the unit queue is dry
   uint32_t steal_max;            // stacked entries a lane may take from busy lanes per launch
   uint32_t run_at;               // run budget once n_in >= run_at/8 of the resident lanes
+  uint32_t mid_budget;           // budget while run_at/8 <= n_in/lanes < full_at/8 (0: run budget)
+  uint32_t full_at;
   uint32_t evict_max;
   uint32_t half_m;
   uint32_t coop_slot;            // lanes per pending owner in the cooperative phase (pow2)
@@ -333,6 +335,18 @@ __device__ __forceinline__ void key_prefix_bit(uint32_t (&K)[MW], uint32_t de) {
     K[w] &= keep;
     if ((de >> 5) == (uint32_t)w) K[w] |= 0x80000000u >> (de & 31u);
   }
+}
+
+// Per-lane node budget of a launch from how well its input covers the resident lanes:
+// a small frontier grows (a few nodes per lane, then spill: more units next launch); a
+// frontier that covers most lanes runs long.  The middle tier (mid_budget, off when 0)
+// bounds launches that would otherwise run with part of the lanes idle.
+__device__ __forceinline__ uint32_t launch_budget(const SearchArgs& a, uint32_t n_in) {
+  const uint64_t lanes8 = (uint64_t)gridDim.x * WAVE;
+  const uint64_t n8 = (uint64_t)n_in * 8u;
+  if (n8 < lanes8 * a.run_at) return a.grow_budget;
+  if (a.mid_budget && n8 < lanes8 * a.full_at) return a.mid_budget;
+  return a.run_budget;
 }
 
 // Wave-aggregated reservation of n (per lane, n < 2^NB) slots on a global counter: the
@@ -484,7 +498,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     if (stop || blockIdx.x >= nb_used) return;
   }
   uint32_t* const records = a.records + (size_t)log_base * RL::WORDS;
-  const uint32_t budget = ((uint64_t)n_in * 8u >= (uint64_t)gridDim.x * WAVE * a.run_at) ? a.run_budget : a.grow_budget;
+  const uint32_t budget = launch_budget(a, n_in);
 #ifdef QI_GSTACK
 #define ST_IDX(lvl, w, ln) ((((ln) * SMAX) + (lvl)) * SE + (w))
 #else
