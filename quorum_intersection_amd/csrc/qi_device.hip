@@ -158,16 +158,21 @@ struct GlobalDev {
   const uint32_t* root;
 };
 
+// GS = true: the per-query state lives in global memory (`scratch`, `per` bytes per
+// query) instead of LDS, for networks whose image exceeds the LDS (a one-wave workgroup
+// sees its own global stores in order; __syncthreads() orders them like LDS ones).
+template <bool GS>
 __global__ __launch_bounds__(64) void gfp_batch_kernel(GlobalDev g, const unsigned long long* nodes,
                                                         const unsigned long long* avail, uint32_t count,
-                                                        unsigned long long* out, unsigned long long* rounds_out) {
+                                                        unsigned long long* out, unsigned long long* rounds_out,
+                                                        uint8_t* scratch, size_t per) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long sm[];
-  unsigned long long* A = sm;             // [words] available set (changes as X shrinks)
+  const uint32_t q = blockIdx.x;
+  if (q >= count) return;
+  unsigned long long* A = GS ? (unsigned long long*)(scratch + (size_t)q * per) : sm;  // [words] available set
   unsigned long long* X = A + g.words;    // [words] current candidates
   uint8_t* sat = (uint8_t*)(X + g.words); // [T]
   const uint32_t lane = threadIdx.x;
-  const uint32_t q = blockIdx.x;
-  if (q >= count) return;
   const unsigned long long* qn = nodes + (size_t)q * g.words;
   const unsigned long long* qa = avail + (size_t)q * g.words;
   for (uint32_t w = lane; w < g.words; w += WAVE) {
@@ -365,7 +370,12 @@ template <typename T>
 T* dalloc(size_t count) {
   void* p = nullptr;
   if (count == 0) count = 1;
-  HIP_CHECK(hipMalloc(&p, count * sizeof(T)));
+  const hipError_t e = hipMalloc(&p, count * sizeof(T));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // not sticky for later calls
+    throw Error(e == hipErrorOutOfMemory ? QI_ERR_CAPACITY : QI_ERR_DEVICE,
+                "hipMalloc(" + std::to_string(count * sizeof(T)) + " B): " + hipGetErrorString(e));
+  }
   return (T*)p;
 }
 
@@ -414,6 +424,7 @@ class GfpDeviceImpl : public GfpDevice {
     for (auto* p : bufs_) (void)hipFree((void*)p);
     (void)hipFree(rounds_);
     (void)hipFree(io_);
+    (void)hipFree(scratch_);
     if (hio_) (void)hipHostFree(hio_);
     (void)hipEventDestroy(e0_);
     (void)hipEventDestroy(e1_);
@@ -439,9 +450,20 @@ class GfpDeviceImpl : public GfpDevice {
     HIP_CHECK(hipMemcpyAsync(dn, hio_, 2 * per * 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(rounds_, 0, 8, stream_));
     const size_t shm = (size_t)d_.words * 16 + ((d_.T + 15) / 16) * 16;
-    if (shm > 160 * 1024) throw Error(QI_ERR_UNSUPPORTED, "gfp_batch: FBAS too large for LDS staging");
     HIP_CHECK(hipEventRecord(e0_, stream_));
-    hipLaunchKernelGGL(dev::gfp_batch_kernel, dim3(count), dim3(64), shm, stream_, d_, dn, da, count, dout, rounds_);
+    if (shm <= kLdsImage) {
+      hipLaunchKernelGGL(dev::gfp_batch_kernel<false>, dim3(count), dim3(64), shm, stream_, d_, dn, da, count, dout,
+                         rounds_, nullptr, (size_t)0);
+    } else {  // a network too large for the LDS image: the same kernel on global scratch
+      const size_t need = shm * count;
+      if (scratch_cap_ < need) {
+        (void)hipFree(scratch_);
+        scratch_ = dalloc<uint8_t>(need);
+        scratch_cap_ = need;
+      }
+      hipLaunchKernelGGL(dev::gfp_batch_kernel<true>, dim3(count), dim3(64), 0, stream_, d_, dn, da, count, dout, rounds_,
+                         scratch_, shm);
+    }
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipEventRecord(e1_, stream_));
     HIP_CHECK(hipMemcpyAsync(hio_ + 2 * per, dout, per * 8, hipMemcpyDeviceToHost, stream_));
@@ -463,6 +485,11 @@ class GfpDeviceImpl : public GfpDevice {
   unsigned long long* io_ = nullptr;
   unsigned long long* hio_ = nullptr;  // pinned staging: nodes, avail, out
   size_t io_cap_ = 0;
+  uint8_t* scratch_ = nullptr;  // global-memory query state (networks beyond the LDS image)
+  size_t scratch_cap_ = 0;
+ public:
+  static size_t kLdsImage;      // LDS bytes one query may use (QI_GFP_LDS overrides: tests)
+ private:
   double last_ms_ = 0;
 };
 
@@ -494,6 +521,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_MID_BUDGET")) cfg_.mid_budget = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_FULL_AT")) cfg_.full_at = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
     if (const char* e = std::getenv("QI_COOP_BATCH")) cfg_.coop_batch = (uint32_t)std::atoi(e);
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
@@ -543,19 +571,25 @@ class SearchDeviceImpl : public SearchDevice {
     const size_t ge = f.grp_extra_off.empty() ? 0 : f.grp_extra_off.back();
     keep(d_.grp_extra = dupload(pad_rows(f.grp_extra, ge), stream_));
     lap("tables");
-    for (uint32_t w = 0; w < 8; ++w) scc_mask_[w] = 0;
+    for (uint32_t w = 0; w < 32; ++w) scc_mask_[w] = 0;
     for (uint32_t v = 0; v < f.m; ++v) scc_mask_[v >> 5] |= 1u << (v & 31);
-    for (uint32_t w = 0; w < 8; ++w) d_.scc_mask[w] = scc_mask_[w];
+    for (uint32_t w = 0; w < 32; ++w) d_.scc_mask[w] = scc_mask_[w];
     if (ORD) {  // per-vertex roots, SCC-local adjacency, hash buckets of the global ids
       keep(ord_.vroot = dupload(f.vroot, stream_));
       keep(ord_.adj_off = dupload(f.ladj_off, stream_));
       keep(ord_.adj = dupload(f.ladj, stream_));
-      std::vector<uint16_t> bm((size_t)5 * f.m);
-      for (uint32_t r = 0; r < 5; ++r)
+      std::vector<uint16_t> bm((size_t)dev::kHashSizes * f.m);
+      for (uint32_t r = 0; r < (uint32_t)dev::kHashSizes; ++r)
         for (uint32_t v = 0; v < f.m; ++v) bm[(size_t)r * f.m + v] = (uint16_t)(f.scc[v] % dev::kHashBuckets[r]);
       keep(ord_.bktmod = dupload(bm, stream_));
       ord_.smax = kOrdSmax;
       ord_.depth_max = 32u * MW;
+      // monotone (here for its size, or forced): sweep order is immaterial; QI_ORDERED=2
+      // keeps the exact sweeps anyway (diagnostics: exercises them on monotone inputs)
+      const char* fo = std::getenv("QI_ORDERED");
+      ord_.jacobi = (f.nonmonotone || (fo && std::atoi(fo) == 2)) ? 0u : 1u;
+      ord_.probe = 2048;
+      if (const char* e = std::getenv("QI_PROBE")) ord_.probe = (uint32_t)std::atoi(e);
     }
 
     cus_ = (uint32_t)device_cu_count(device_);
@@ -595,8 +629,11 @@ class SearchDeviceImpl : public SearchDevice {
       if (ORD) nb = std::min(nb, 8);  // scratch-heavy lanes: a few waves per CU hide the latency
       if (nb > 0) max_blocks_ = cus_ * (uint32_t)nb;
     }
-    if (ORD)  // one DFS stack per lane of every block of a launch
-      keep(ord_.ostack = dalloc<uint32_t>((size_t)max_blocks_ * kOrdSmax * (dev::OrdUnitLayout<MW>::OWT + 2) * 64));
+    if (ORD) {  // one DFS stack (and, beyond 256 vertices, one workspace) per lane of a launch
+      keep(ord_.ostack = dalloc<uint32_t>((size_t)max_blocks_ * kOrdSmax * (dev::OrdUnitLayout<MW>::OWT + 3) * 64));
+      if (dev::OrdWorkspace<MW>::GLOBAL)
+        keep(ord_.ows = dalloc<uint8_t>((size_t)max_blocks_ * 64 * dev::OrdWorkspace<MW>::BYTES));
+    }
     lap("occupancy");
     if ((cfg_.jit == 0 || cfg_.jit == 4) && jit_eligible(flat_)) {
       // auto / cache-only: a specialised kernel already in the on-disk cache runs from the
@@ -650,7 +687,7 @@ class SearchDeviceImpl : public SearchDevice {
     std::vector<uint32_t> u(UL::WORDS, 0);
     if constexpr (ORD) {  // toRemove = scc in ascending order, dontRemove = {} (cpp:393)
       u[UL::TLEN] = m_;
-      for (uint32_t v = 0; v < m_; ++v) u[UL::TORD + v / 4] |= v << (8 * (v % 4));
+      for (uint32_t v = 0; v < m_; ++v) u[UL::TORD + v / UL::EPW] |= v << (32 / UL::EPW * (v % UL::EPW));
     } else {
       for (int w = 0; w < MW; ++w) u[UL::T_ + w] = scc_mask_[w];  // toRemove = scc, dontRemove = {} (cpp:393)
     }
@@ -837,10 +874,13 @@ class SearchDeviceImpl : public SearchDevice {
     }
     if (g_flags & dev::FLAG_POOL) {  // some lane found the eviction pool dry and stopped early:
       // double the frontier buffers (the current frontier is preserved), so the next
-      // launches can dig deeper
+      // launches can dig deeper -- up to the frontier memory budget: past it lanes keep
+      // spilling and stopping, which the preorder sort after a halt keeps progressing
       const uint64_t c2 = 2 * std::min(cap_[0], cap_[1]);
-      ensure_cap(cur_, c2, true);
-      ensure_cap(1 - cur_, c2);
+      if (2 * c2 * (uint64_t)UL::BYTES <= max_frontier_bytes_) {
+        ensure_cap(cur_, c2, true);
+        ensure_cap(1 - cur_, c2);
+      }
       const uint32_t zero = 0;
       HIP_CHECK(hipMemcpyAsync(glob_ + 1, &zero, 4, hipMemcpyHostToDevice, stream_));
       HIP_CHECK(hipStreamSynchronize(stream_));
@@ -1125,7 +1165,8 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t dl = wv[MW + 1];
     for (uint32_t v = 0; v < m_; ++v)
       if ((wv[MW + 2 + (v >> 5)] >> (v & 31)) & 1u) w.q1_local.push_back(v);
-    for (uint32_t i = 0; i < dl; ++i) w.q2_local.push_back((wv[2 * MW + 2 + i / 4] >> (8 * (i % 4))) & 255u);
+    constexpr uint32_t EPW = 4 / dev::OrdBytes<MW>::VB, EB = 32 / EPW;
+    for (uint32_t i = 0; i < dl; ++i) w.q2_local.push_back((wv[2 * MW + 2 + i / EPW] >> (EB * (i % EPW))) & ((1u << EB) - 1u));
     if (!has_local_best_ || key_less(w.key, w.depth, local_best_.key, local_best_.depth)) {
       local_best_ = w;
       has_local_best_ = true;
@@ -1140,7 +1181,7 @@ class SearchDeviceImpl : public SearchDevice {
   hipEvent_t e0_{}, e1_{};
   dev::LocalDev d_{};
   std::vector<void*> bufs_;
-  uint32_t scc_mask_[8];
+  uint32_t scc_mask_[32];
   uint32_t max_blocks_ = 0;
   uint32_t cus_ = 0;
   uint32_t* units_[2] = {nullptr, nullptr};
@@ -1148,6 +1189,7 @@ class SearchDeviceImpl : public SearchDevice {
   int cur_ = 0;
   uint64_t n_ = 0;
   uint32_t idle_steps_ = 0;    // consecutive steps without progress (guard)
+  uint64_t max_frontier_bytes_ = 16ull << 30;  // both frontier buffers (QI_MAX_FRONTIER_GB)
   uint64_t pool_growths_ = 0;  // buffer doublings after a dry eviction pool
   static constexpr uint32_t kMaxBatch = 64;
   uint32_t* ctr_ = nullptr;       // [kMaxBatch + 1][CTR_WORDS]: seed block + one per launch
@@ -1230,8 +1272,8 @@ class SearchDeviceImpl : public SearchDevice {
 // vertex v; the table is built by inserting seq[0..n_seq) in order (repeats ignored).
 uint32_t hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint32_t* seq, uint32_t n_seq,
                               uint32_t* out) {
-  if (n_keys > 256) throw Error(QI_ERR_ARG, "hash order: more than 256 keys");
-  auto* hl = new dev::HashList<256, 257>;
+  if (n_keys > 1024) throw Error(QI_ERR_ARG, "hash order: more than 1024 keys");
+  auto* hl = new dev::HashList<1024, 1109>;
   hl->clear();
   std::vector<uint8_t> seen(n_keys, 0);
   auto bmod = [&](uint32_t v, int r) -> uint32_t { return keys[v] % dev::kHashBuckets[r]; };
@@ -1246,12 +1288,15 @@ uint32_t hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint3
     hl->insert((uint16_t)v, bmod);
   }
   uint32_t n = 0;
-  for (uint16_t v = hl->head; v != dev::HashList<256, 257>::NIL; v = hl->nxt[v]) out[n++] = v;
+  for (uint16_t v = hl->head; v != dev::HashList<1024, 1109>::NIL; v = hl->nxt[v]) out[n++] = v;
   delete hl;
   return n;
 }
 
+size_t GfpDeviceImpl::kLdsImage = 160 * 1024;
+
 std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g) {
+  if (const char* e = std::getenv("QI_GFP_LDS")) GfpDeviceImpl::kLdsImage = (size_t)std::atoll(e);
   return std::unique_ptr<GfpDevice>(new GfpDeviceImpl(device, g));
 }
 
@@ -1272,26 +1317,31 @@ bool jit_precompile(const LocalFlat& f, std::string* log) {
 }
 
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg) {
+  using P = std::unique_ptr<SearchDevice>;
   const uint32_t mw = f.mw, tw = f.tw;
-  // threshold-0 quorum sets: the order-exact kernel (QI_ORDERED=1 forces it, diagnostics)
+  // threshold-0 quorum sets: the order-exact kernel (QI_ORDERED=1 forces it, diagnostics);
+  // |SCC| or the TN count beyond 256: the order-exact kernel too (exact for monotone SCCs
+  // as well), with 16-bit order lists
   const char* fo = std::getenv("QI_ORDERED");
-  if (f.nonmonotone || (fo && std::atoi(fo) != 0)) {
-    if (mw <= 1 && tw <= 1) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 1, 24, true>(device, f, cfg));
-    if (mw <= 1 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 4, 24, true>(device, f, cfg));
-    if (mw <= 2 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<2, 4, 16, true>(device, f, cfg));
-    if (mw <= 4 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<4, 8, 12, true>(device, f, cfg));
-    if (mw <= 8 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<8, 8, 8, true>(device, f, cfg));
-    throw Error(QI_ERR_UNSUPPORTED, "searched SCC too large for the device kernels (|SCC| > 256 or > 256 TNs)");
+  const bool ordered = f.nonmonotone || (fo && std::atoi(fo) != 0) || mw > 8 || tw > 8;
+  if (ordered) {
+    if (mw <= 1 && tw <= 1) return P(new SearchDeviceImpl<1, 1, 24, true>(device, f, cfg));
+    if (mw <= 1 && tw <= 4) return P(new SearchDeviceImpl<1, 4, 24, true>(device, f, cfg));
+    if (mw <= 2 && tw <= 4) return P(new SearchDeviceImpl<2, 4, 16, true>(device, f, cfg));
+    if (mw <= 4 && tw <= 8) return P(new SearchDeviceImpl<4, 8, 12, true>(device, f, cfg));
+    if (mw <= 8 && tw <= 8) return P(new SearchDeviceImpl<8, 8, 8, true>(device, f, cfg));
+    if (mw <= 16 && tw <= 16) return P(new SearchDeviceImpl<16, 16, 8, true>(device, f, cfg));
+    if (mw <= 32 && tw <= 32) return P(new SearchDeviceImpl<32, 32, 8, true>(device, f, cfg));
+    throw Error(QI_ERR_UNSUPPORTED, "searched SCC too large for the device kernels (|SCC| > 1024 or > 1024 TNs)");
   }
-  if (mw <= 1 && tw <= 1) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 1, 24>(device, f, cfg));
-  if (mw <= 1 && tw <= 2) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 2, 24>(device, f, cfg));
-  if (mw <= 1 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<1, 4, 24>(device, f, cfg));
-  if (mw <= 2 && tw <= 2) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<2, 2, 16>(device, f, cfg));
-  if (mw <= 2 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<2, 4, 16>(device, f, cfg));
-  if (mw <= 4 && tw <= 4) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<4, 4, 12>(device, f, cfg));
-  if (mw <= 4 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<4, 8, 12>(device, f, cfg));
-  if (mw <= 8 && tw <= 8) return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<8, 8, 8>(device, f, cfg));
-  throw Error(QI_ERR_UNSUPPORTED, "searched SCC too large for the device kernels (|SCC| > 256 or > 256 TNs)");
+  if (mw <= 1 && tw <= 1) return P(new SearchDeviceImpl<1, 1, 24>(device, f, cfg));
+  if (mw <= 1 && tw <= 2) return P(new SearchDeviceImpl<1, 2, 24>(device, f, cfg));
+  if (mw <= 1 && tw <= 4) return P(new SearchDeviceImpl<1, 4, 24>(device, f, cfg));
+  if (mw <= 2 && tw <= 2) return P(new SearchDeviceImpl<2, 2, 16>(device, f, cfg));
+  if (mw <= 2 && tw <= 4) return P(new SearchDeviceImpl<2, 4, 16>(device, f, cfg));
+  if (mw <= 4 && tw <= 4) return P(new SearchDeviceImpl<4, 4, 12>(device, f, cfg));
+  if (mw <= 4 && tw <= 8) return P(new SearchDeviceImpl<4, 8, 12>(device, f, cfg));
+  return P(new SearchDeviceImpl<8, 8, 8>(device, f, cfg));
 }
 
 }  // namespace qi

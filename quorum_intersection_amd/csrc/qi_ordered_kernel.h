@@ -42,10 +42,15 @@ namespace dev {
 // new buckets.  Erasing (cpp:321-323) unlinks without reordering, so the iteration order
 // of the survivors is the list order restricted to them.
 // ------------------------------------------------------------------------------------
-constexpr uint32_t kHashBuckets[5] = {13u, 29u, 59u, 127u, 257u};
+constexpr uint32_t kHashBuckets[7] = {13u, 29u, 59u, 127u, 257u, 541u, 1109u};
+constexpr int kHashSizes = 7;
 
 __host__ __device__ inline int hash_grow_at(uint32_t k) {  // k-th distinct insertion (1-based)
-  return k == 1u ? 0 : k == 14u ? 1 : k == 30u ? 2 : k == 60u ? 3 : k == 128u ? 4 : -1;
+  return k == 1u ? 0 : k == 14u ? 1 : k == 30u ? 2 : k == 60u ? 3 : k == 128u ? 4 : k == 258u ? 5 : k == 542u ? 6 : -1;
+}
+// buckets needed for up to CAP distinct elements
+constexpr int hash_buckets_for(int cap) {
+  return cap < 14 ? 13 : cap < 30 ? 29 : cap < 60 ? 59 : cap < 128 ? 127 : cap < 258 ? 257 : cap < 542 ? 541 : 1109;
 }
 
 // CAP: elements (local vertex ids < CAP), NB: bucket capacity.  bmod(v, r) = key(v) %
@@ -121,13 +126,15 @@ struct HashList {
 
 // ------------------------------------------------------------------------------------
 // Ordered unit: path key, depth, |D| (with repetitions), |toRemove|, D in branch order,
-// toRemove in hash order (one byte per local vertex).
+// toRemove in hash order (OrdBytes<MW>::VB bytes per local vertex: 1 up to 256 vertices).
 // ------------------------------------------------------------------------------------
 template <int MW>
 struct OrdUnitLayout {
+  static constexpr int VB = OrdBytes<MW>::VB;
+  static constexpr int EPW = 4 / VB;        // entries per 32-bit word
   static constexpr int DMAX = MW * 16 + 1;  // |D| <= m/2 + 1
-  static constexpr int OWD = (DMAX + 3) / 4;
-  static constexpr int OWT = MW * 8;        // up to 32*MW toRemove bytes
+  static constexpr int OWD = (DMAX + EPW - 1) / EPW;
+  static constexpr int OWT = MW * 32 / EPW; // up to 32*MW toRemove entries
   static constexpr int K_ = 0, DEPTH = MW, DLEN = MW + 1, TLEN = MW + 2, DORD = MW + 3, TORD = MW + 3 + OWD;
   static constexpr int RAW = MW + 3 + OWD + OWT;
   static constexpr int WORDS = (RAW + 3) / 4 * 4;
@@ -141,16 +148,35 @@ struct OrdArgs {
   const uint32_t* vroot;    // [m] root TN of each local vertex, 0xFFFFFFFF: never satisfied
   const uint32_t* adj_off;  // [m+1] out-edges inside the SCC, with multiplicity (cpp:222-247)
   const uint32_t* adj;
-  const uint16_t* bktmod;   // [5][m] global vertex index % kHashBuckets[r]
+  const uint16_t* bktmod;   // [kHashSizes][m] global vertex index % kHashBuckets[r]
   uint32_t* ostack;         // [blocks][smax][SEW][64] per-lane DFS stacks
+  uint8_t* ows;             // MW > 8: per-lane workspace [blocks * 64][OrdWorkspace<MW>::BYTES]
   uint32_t smax;
   uint32_t depth_max;       // < 32*MW: path keys hold one bit per level
+  uint32_t jacobi;          // 1: monotone SCC (here only for its size): Jacobi rounds give the
+                            // same survivor set as any sweep order, and far fewer TN passes
+  uint32_t probe;           // node budget of the root's lane while the frontier is the root
+                            // alone: a depth-first probe before the parallel expansion
 };
 
 // TN satisfaction bits under availability A (inside the SCC; POL as in gfp)
 template <int MW, int TW, int POL>
 __device__ __forceinline__ void tn_sat(const LocalDev& f, const uint32_t (&A)[MW], uint32_t (&sb)[TW]) {
   using R = TnRec<MW, TW>;
+  if constexpr (TW > 8) {  // |SCC| or TNs beyond 256: rolled loops, dynamic word indexing
+    for (int w = 0; w < TW; ++w) sb[w] = 0;
+    const __attribute__((address_space(4))) uint32_t* rec = K(f.tn);
+    for (uint32_t t = 0; t < f.T; ++t, rec += R::WORDS) {
+      uint32_t c = 0;
+      for (int w = 0; w < MW; ++w) c += __popc(A[w] & rec[w]);
+      for (uint32_t w = 0; w <= (t >> 5); ++w) c += __popc(sb[w] & rec[MW + w]);
+      if (rec[R::EXTRA]) c += extra_terms<MW, TW>(f, t, A, sb);
+      const int32_t th = POL == 0 ? (int32_t)rec[R::THR0] : (int32_t)rec[R::THR1];
+      const uint32_t bit = (((int32_t)c >= th) ? 1u : 0u) ^ rec[R::INV];
+      sb[t >> 5] |= bit << (t & 31u);
+    }
+    return;
+  }
 #pragma unroll
   for (int w = 0; w < TW; ++w) sb[w] = 0;
 #pragma unroll
@@ -174,6 +200,7 @@ __device__ __forceinline__ void tn_sat(const LocalDev& f, const uint32_t (&A)[MW
 
 template <int MW>
 __device__ __forceinline__ bool mbit(const uint32_t (&X)[MW], uint32_t v) {
+  if constexpr (MW > 8) return (X[v >> 5] >> (v & 31u)) & 1u;
   uint32_t w = X[0];
 #pragma unroll
   for (int i = 1; i < MW; ++i) w = ((v >> 5) == (uint32_t)i) ? X[i] : w;
@@ -181,6 +208,10 @@ __device__ __forceinline__ bool mbit(const uint32_t (&X)[MW], uint32_t v) {
 }
 template <int MW>
 __device__ __forceinline__ void mset(uint32_t (&X)[MW], uint32_t v, bool on) {
+  if constexpr (MW > 8) {
+    X[v >> 5] = on ? (X[v >> 5] | (1u << (v & 31u))) : (X[v >> 5] & ~(1u << (v & 31u)));
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < MW; ++i)
     if ((v >> 5) == (uint32_t)i) X[i] = on ? (X[i] | (1u << (v & 31u))) : (X[i] & ~(1u << (v & 31u)));
@@ -190,10 +221,49 @@ __device__ __forceinline__ void mset(uint32_t (&X)[MW], uint32_t v, bool on) {
 // a failing vertex leaves the list and (if available) the availability set at once.
 // L[0..len) is filtered in place (survivors keep their order); A is the caller's
 // availability (the reference restores it afterwards, cpp:171-173, so it is copied).
-template <int MW, int TW, int POL>
-__device__ uint32_t gs_fixpoint(const LocalDev& f, const uint32_t* vroot, uint8_t* L, uint32_t len,
-                                const uint32_t (&A0)[MW], uint32_t& rounds) {
+template <int MW, int TW, int POL, typename V>
+__device__ uint32_t gs_fixpoint(const LocalDev& f, const uint32_t* vroot, V* L, uint32_t len,
+                                const uint32_t (&A0)[MW], uint32_t& rounds, bool jacobi) {
   uint32_t A[MW], sb[TW];
+  if (jacobi) {
+    // monotone slices: X = listed and available, X <- X ∩ sat(X) until stable; the
+    // survivors keep their list order (cpp:156 filters in order)
+    uint32_t X[MW];
+#pragma unroll
+    for (int w = 0; w < MW; ++w) X[w] = 0;
+    for (uint32_t i = 0; i < len; ++i)
+      if (mbit<MW>(A0, L[i])) mset<MW>(X, L[i], true);
+    for (;;) {
+      ++rounds;
+      tn_sat<MW, TW, POL>(f, X, sb);
+      bool changed = false;
+      for (uint32_t i = 0; i < len; ++i) {
+        const uint32_t v = L[i];
+        if (!mbit<MW>(X, v)) continue;
+        const uint32_t rt = vroot[v];
+        bool ok = rt != 0xFFFFFFFFu;
+        if (ok) {
+          uint32_t word = sb[0];
+          if constexpr (TW > 8) {
+            word = sb[rt >> 5];
+          } else {
+#pragma unroll
+            for (int w = 1; w < TW; ++w) word = ((rt >> 5) == (uint32_t)w) ? sb[w] : word;
+          }
+          ok = (word >> (rt & 31u)) & 1u;
+        }
+        if (!ok) {
+          mset<MW>(X, v, false);
+          changed = true;
+        }
+      }
+      if (!changed) break;
+    }
+    uint32_t o = 0;
+    for (uint32_t i = 0; i < len; ++i)
+      if (mbit<MW>(X, L[i])) L[o++] = L[i];
+    return o;
+  }
 #pragma unroll
   for (int w = 0; w < MW; ++w) A[w] = A0[w];
   bool sb_ok = false;
@@ -214,8 +284,12 @@ __device__ uint32_t gs_fixpoint(const LocalDev& f, const uint32_t* vroot, uint8_
             sb_ok = true;
           }
           uint32_t word = sb[0];
+          if constexpr (TW > 8) {
+            word = sb[rt >> 5];
+          } else {
 #pragma unroll
-          for (int w = 1; w < TW; ++w) word = ((rt >> 5) == (uint32_t)w) ? sb[w] : word;
+            for (int w = 1; w < TW; ++w) word = ((rt >> 5) == (uint32_t)w) ? sb[w] : word;
+          }
           ok = (word >> (rt & 31u)) & 1u;
         }
         if (!ok) {  // cpp:157-161: unavailable from here on, for the rest of the sweep too
@@ -223,7 +297,7 @@ __device__ uint32_t gs_fixpoint(const LocalDev& f, const uint32_t* vroot, uint8_
           sb_ok = false;
         }
       }
-      if (ok) L[o++] = (uint8_t)v;
+      if (ok) L[o++] = (V)v;
       else dropped = true;
     }
     len = o;
@@ -232,6 +306,24 @@ __device__ uint32_t gs_fixpoint(const LocalDev& f, const uint32_t* vroot, uint8_
   return len;
 }
 
+// Per-lane lists, degree counters and hash table.  Up to 256 vertices they are private
+// (scratch) arrays; beyond, a lane needs ~13 KB, and private segments that large exceed
+// what the runtime reserves for every possible wave, so they live in an explicit global
+// workspace (OrdArgs::ows) instead.
+template <int MW>
+struct OrdWorkspace {
+  static constexpr bool GLOBAL = MW > 8;
+  static constexpr int CAP = 32 * MW, DMAX = MW * 16 + 1, VB = OrdBytes<MW>::VB;
+  static constexpr int R16(int b) { return (b + 15) / 16 * 16; }
+  static constexpr int OFF_D = 0;
+  static constexpr int OFF_T = OFF_D + R16(DMAX * VB);
+  static constexpr int OFF_L = OFF_T + R16(CAP * VB);
+  static constexpr int OFF_G = OFF_L + R16((CAP + DMAX) * VB);
+  static constexpr int OFF_H = OFF_G + R16(CAP * 2);
+  static constexpr int BYTES = OFF_H + R16((int)sizeof(HashList<CAP, hash_buckets_for(CAP)>));
+};
+struct OrdEmpty {};
+
 template <int MW, int TW>
 __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
   using UL = OrdUnitLayout<MW>;
@@ -239,8 +331,11 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
   using WL = WitLayout<MW>;
   constexpr int DMAX = UL::DMAX;
   constexpr int CAP = 32 * MW;            // local vertices
-  constexpr int NB = MW == 1 ? 59 : (MW == 2 ? 127 : 257);  // buckets for <= CAP elements
-  constexpr int SEW = UL::OWT + 2;        // stack entry: T' bytes | b, |T'|, |D| | depth
+  constexpr int NB = hash_buckets_for(CAP);
+  constexpr int SEW = UL::OWT + 3;        // stack entry: T' entries | b, |D| | depth | |T'|
+  constexpr int EPW = UL::EPW, EB = 32 / EPW;  // entries per word, bits per entry
+  constexpr uint32_t EMASK = (1u << EB) - 1u;
+  using V = std::conditional_t<(UL::VB == 2), uint16_t, uint8_t>;
   const SearchArgs& a = oa.a;
   const LocalDev& f = a.f;
   const uint32_t lane = threadIdx.x;
@@ -285,7 +380,10 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     if (stop || blockIdx.x >= nb_used) return;
   }
   uint32_t* const records = a.records + (size_t)log_base * RL::WORDS;
-  const uint32_t budget = launch_budget(a, n_in);
+  // a lone root unit first goes depth-first on one lane: an early witness (cpp:369-377)
+  // then ends the search before the parallel growth expands the subtrees after it
+  const bool probing = n_in == 1u && oa.probe;  // (no grace: nothing else is left to claim)
+  const uint32_t budget = probing ? oa.probe : launch_budget(a, n_in);
   uint32_t* const st = oa.ostack + (size_t)blockIdx.x * (oa.smax * SEW * WAVE);
 #define OST(lvl, w) st[((size_t)(lvl) * SEW + (w)) * WAVE + lane]
 
@@ -296,11 +394,35 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
 #pragma unroll
   for (int w = 0; w < MW; ++w) K[w] = 0;
   uint32_t depth = 0, dlen = 0, tlen = 0;
-  uint8_t Dord[DMAX];
-  uint8_t Tord[CAP];
-  uint8_t Lst[CAP + DMAX];
-  uint16_t deg[CAP];
-  HashList<CAP, NB> hl;
+  using WS = OrdWorkspace<MW>;
+  using HL = HashList<CAP, NB>;
+  using DArr = V[DMAX];
+  using TArr = V[CAP];
+  using LArr = V[CAP + DMAX];
+  using GArr = uint16_t[CAP];
+  std::conditional_t<WS::GLOBAL, OrdEmpty, DArr> d_store;
+  std::conditional_t<WS::GLOBAL, OrdEmpty, TArr> t_store;
+  std::conditional_t<WS::GLOBAL, OrdEmpty, LArr> l_store;
+  std::conditional_t<WS::GLOBAL, OrdEmpty, GArr> g_store;
+  std::conditional_t<WS::GLOBAL, OrdEmpty, HL> h_store;
+  V *Dord, *Tord, *Lst;
+  uint16_t* deg;
+  HL* hlp;
+  if constexpr (WS::GLOBAL) {
+    uint8_t* w = oa.ows + ((size_t)blockIdx.x * WAVE + lane) * WS::BYTES;
+    Dord = (V*)(w + WS::OFF_D);
+    Tord = (V*)(w + WS::OFF_T);
+    Lst = (V*)(w + WS::OFF_L);
+    deg = (uint16_t*)(w + WS::OFF_G);
+    hlp = (HL*)(w + WS::OFF_H);
+  } else {
+    Dord = (V*)&d_store;
+    Tord = (V*)&t_store;
+    Lst = (V*)&l_store;
+    deg = (uint16_t*)&g_store;
+    hlp = (HL*)&h_store;
+  }
+  HL& hl = *hlp;
   bool has = false, done = false;
   uint32_t nst = 0, sbase = 0;
   auto spos = [&](uint32_t i) -> uint32_t {
@@ -338,9 +460,9 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     if (MW > 1 && a.has_best) p = after_key<MW>(KK, d, a.best_key, a.best_depth);
     return p || (best_pack<MW>(KK, d) > best64);
   };
-  // unit writers: D order = Dord[0..dl) (+ extra byte b >= 0), T order = tb[0..tl)
+  // unit writers: D order = Dord[0..dl) (+ extra entry b >= 0), T order = tb[0..tl)
   auto write_unit = [&](uint32_t slot, const uint32_t (&UK)[MW], uint32_t udepth, uint32_t dl, int b,
-                        const uint8_t* tb, uint32_t tl, bool t_from_stack, uint32_t spos_) {
+                        const V* tb, uint32_t tl, bool t_from_stack, uint32_t spos_) {
     if (slot >= a.out_cap) {
       atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
       return;
@@ -352,29 +474,29 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     u[UL::DEPTH] = udepth;
     u[UL::DLEN] = ul;
     u[UL::TLEN] = tl;
-    for (uint32_t i = 0; i < (ul + 3u) / 4u; ++i) {
+    for (uint32_t i = 0; i < (ul + EPW - 1u) / EPW; ++i) {
       uint32_t word = 0;
-      for (uint32_t j = 0; j < 4u; ++j) {
-        const uint32_t p = 4u * i + j;
-        const uint32_t byte = p < dl ? Dord[p] : (p == dl && b >= 0 ? (uint32_t)b : 0u);
-        word |= byte << (8u * j);
+      for (uint32_t j = 0; j < (uint32_t)EPW; ++j) {
+        const uint32_t p = EPW * i + j;
+        const uint32_t e = p < dl ? (uint32_t)Dord[p] : (p == dl && b >= 0 ? (uint32_t)b : 0u);
+        word |= e << (EB * j);
       }
       u[UL::DORD + i] = word;
     }
     if (t_from_stack) {
-      for (uint32_t i = 0; i < (tl + 3u) / 4u; ++i) u[UL::TORD + i] = OST(spos_, i);
+      for (uint32_t i = 0; i < (tl + EPW - 1u) / EPW; ++i) u[UL::TORD + i] = OST(spos_, i);
     } else {
-      for (uint32_t i = 0; i < (tl + 3u) / 4u; ++i) {
+      for (uint32_t i = 0; i < (tl + EPW - 1u) / EPW; ++i) {
         uint32_t word = 0;
-        for (uint32_t j = 0; j < 4u && 4u * i + j < tl; ++j) word |= (uint32_t)tb[4u * i + j] << (8u * j);
+        for (uint32_t j = 0; j < (uint32_t)EPW && EPW * i + j < tl; ++j) word |= (uint32_t)tb[EPW * i + j] << (EB * j);
         u[UL::TORD + i] = word;
       }
     }
   };
   // stack entry at circular position p as a unit (the inclusion child it stands for)
   auto write_entry = [&](uint32_t slot, uint32_t p) {
-    const uint32_t pk = OST(p, UL::OWT), de = OST(p, UL::OWT + 1);
-    const uint32_t b = pk & 255u, tl = (pk >> 8) & 511u, dle = pk >> 17;
+    const uint32_t pk = OST(p, UL::OWT), de = OST(p, UL::OWT + 1), tl = OST(p, UL::OWT + 2);
+    const uint32_t b = pk & 0xFFFFu, dle = pk >> 16;
     uint32_t UK[MW];
 #pragma unroll
     for (int w = 0; w < MW; ++w) UK[w] = K[w];
@@ -388,7 +510,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     const uint32_t idx = static_end + h;
     if (idx >= n_in) {
       dry = true;
-      limit = min(limit, steps + a.grace);
+      if (!probing) limit = min(limit, steps + a.grace);
       return false;
     }
     seg_idx = idx;
@@ -401,8 +523,8 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     depth = seg_depth = u[UL::DEPTH];
     dlen = u[UL::DLEN];
     tlen = u[UL::TLEN];
-    for (uint32_t i = 0; i < dlen; ++i) Dord[i] = (uint8_t)(u[UL::DORD + (i >> 2)] >> (8u * (i & 3u)));
-    for (uint32_t i = 0; i < tlen; ++i) Tord[i] = (uint8_t)(u[UL::TORD + (i >> 2)] >> (8u * (i & 3u)));
+    for (uint32_t i = 0; i < dlen; ++i) Dord[i] = (V)((u[UL::DORD + i / EPW] >> (EB * (i % EPW))) & EMASK);
+    for (uint32_t i = 0; i < tlen; ++i) Tord[i] = (V)((u[UL::TORD + i / EPW] >> (EB * (i % EPW))) & EMASK);
     seg_idx = idx;
     seg_open = true;
     seg_count = seg_evals = seg_minq = seg_zfb = 0;
@@ -419,7 +541,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     if (!has) {
       if (nst > 0) {
         const uint32_t p = spos(nst - 1u);
-        const uint32_t pk = OST(p, UL::OWT), de = OST(p, UL::OWT + 1);
+        const uint32_t pk = OST(p, UL::OWT), de = OST(p, UL::OWT + 1), tl = OST(p, UL::OWT + 2);
         uint32_t NK[MW];
 #pragma unroll
         for (int w = 0; w < MW; ++w) NK[w] = K[w];
@@ -428,13 +550,13 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
           nst = 0;
         } else {
           --nst;
-          const uint32_t b = pk & 255u, tl = (pk >> 8) & 511u, dle = pk >> 17;
-          for (uint32_t i = 0; i < (tl + 3u) / 4u; ++i) {
+          const uint32_t b = pk & 0xFFFFu, dle = pk >> 16;
+          for (uint32_t i = 0; i < (tl + EPW - 1u) / EPW; ++i) {
             const uint32_t word = OST(p, i);
-            for (uint32_t j = 0; j < 4u && 4u * i + j < tl; ++j) Tord[4u * i + j] = (uint8_t)(word >> (8u * j));
+            for (uint32_t j = 0; j < (uint32_t)EPW && EPW * i + j < tl; ++j) Tord[EPW * i + j] = (V)((word >> (EB * j)) & EMASK);
           }
           tlen = tl;
-          Dord[dle] = (uint8_t)b;
+          Dord[dle] = (V)b;
           dlen = dle + 1u;
           depth = de + 1u;
 #pragma unroll
@@ -461,7 +583,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
       best64 = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!dry && static_end + h >= n_in) {
         dry = true;
-        limit = min(limit, steps + a.grace);
+        if (!probing) limit = min(limit, steps + a.grace);
       }
     }
     // ---- budget / eviction cap: the node and the stack go to the next frontier ----------
@@ -493,7 +615,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     // cpp:275-281: GFP(D), nodes = D in branch order, only D available
     for (uint32_t i = 0; i < dlen; ++i) Lst[i] = Dord[i];
     ++seg_evals;
-    if (gs_fixpoint<MW, TW, 0>(f, oa.vroot, Lst, dlen, Dm, rounds)) {
+    if (gs_fixpoint<MW, TW, 0>(f, oa.vroot, Lst, dlen, Dm, rounds, oa.jacobi != 0)) {
       // cpp:283 isMinimalQuorum: cpp:184 repeats cpp:281 (same inputs, same result)
       ++seg_evals;
       bool minimal = true;
@@ -504,7 +626,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
         mset<MW>(A, Dord[i], false);
         for (uint32_t j = 0; j < dlen; ++j) Lst[j] = Dord[j];
         ++seg_evals;
-        if (gs_fixpoint<MW, TW, 0>(f, oa.vroot, Lst, dlen, A, rounds)) minimal = false;
+        if (gs_fixpoint<MW, TW, 0>(f, oa.vroot, Lst, dlen, A, rounds, oa.jacobi != 0)) minimal = false;
       }
       if (minimal) {  // visitor (cpp:357-384): scc in ascending order, D unavailable
         ++seg_minq;
@@ -512,8 +634,8 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
         uint32_t A[MW];
 #pragma unroll
         for (int w = 0; w < MW; ++w) A[w] = f.scc_mask[w] & ~Dm[w];
-        for (uint32_t v = 0; v < m; ++v) Lst[v] = (uint8_t)v;
-        const uint32_t ql = gs_fixpoint<MW, TW, 1>(f, oa.vroot, Lst, m, A, rounds);
+        for (uint32_t v = 0; v < m; ++v) Lst[v] = (V)v;
+        const uint32_t ql = gs_fixpoint<MW, TW, 1>(f, oa.vroot, Lst, m, A, rounds, oa.jacobi != 0);
         if (ql) {  // cpp:369-377: disjoint quorums, the search ends here
           uint32_t Q1[MW];
 #pragma unroll
@@ -529,9 +651,9 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
             }
             wv[MW] = depth;
             wv[MW + 1] = dlen;
-            for (uint32_t i = 0; i < (dlen + 3u) / 4u; ++i) {
+            for (uint32_t i = 0; i < (dlen + EPW - 1u) / EPW; ++i) {
               uint32_t word = 0;
-              for (uint32_t j = 0; j < 4u && 4u * i + j < dlen; ++j) word |= (uint32_t)Dord[4u * i + j] << (8u * j);
+              for (uint32_t j = 0; j < (uint32_t)EPW && EPW * i + j < dlen; ++j) word |= (uint32_t)Dord[EPW * i + j] << (EB * j);
               wv[2 * MW + 2 + i] = word;
             }
           } else {
@@ -554,7 +676,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
       mset<MW>(A, Tord[i], true);
     }
     ++seg_evals;
-    const uint32_t ql = gs_fixpoint<MW, TW, 0>(f, oa.vroot, Lst, dlen + tlen, A, rounds);
+    const uint32_t ql = gs_fixpoint<MW, TW, 0>(f, oa.vroot, Lst, dlen + tlen, A, rounds, oa.jacobi != 0);
     if (!ql) continue;  // cpp:303
     uint32_t Qm[MW];
 #pragma unroll
@@ -598,7 +720,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     }
     uint32_t tl = 0;
     for (uint16_t v = hl.head; v != HashList<CAP, NB>::NIL; v = hl.nxt[v])
-      if (!mbit<MW>(Dm, v) && v != best) Tord[tl++] = (uint8_t)v;
+      if (!mbit<MW>(Dm, v) && v != best) Tord[tl++] = (V)v;
     tlen = tl;
     // push the inclusion child (cpp:343-345), continue with the exclusion child (cpp:336)
     if (nst == oa.smax) {  // full: the shallowest entry goes to the next frontier
@@ -613,13 +735,14 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     }
     {
       const uint32_t p = spos(nst);
-      for (uint32_t i = 0; i < (tl + 3u) / 4u; ++i) {
+      for (uint32_t i = 0; i < (tl + EPW - 1u) / EPW; ++i) {
         uint32_t word = 0;
-        for (uint32_t j = 0; j < 4u && 4u * i + j < tl; ++j) word |= (uint32_t)Tord[4u * i + j] << (8u * j);
+        for (uint32_t j = 0; j < (uint32_t)EPW && EPW * i + j < tl; ++j) word |= (uint32_t)Tord[EPW * i + j] << (EB * j);
         OST(p, i) = word;
       }
-      OST(p, UL::OWT) = best | (tl << 8) | (dlen << 17);
+      OST(p, UL::OWT) = best | (dlen << 16);
       OST(p, UL::OWT + 1) = depth;
+      OST(p, UL::OWT + 2) = tl;
       ++nst;
     }
     ++depth;

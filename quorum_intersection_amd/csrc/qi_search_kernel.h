@@ -36,7 +36,7 @@ constexpr int WAVE = 64;
 template <int MW, int TW>
 struct TnRec {
   static constexpr int RAW = MW + TW + 4;
-  static constexpr int WORDS = RAW <= 8 ? 8 : (RAW <= 16 ? 16 : 32);
+  static constexpr int WORDS = RAW <= 8 ? 8 : (RAW <= 16 ? 16 : (RAW <= 32 ? 32 : (RAW <= 64 ? 64 : 128)));
   static constexpr int THR0 = MW + TW, THR1 = MW + TW + 1, INV = MW + TW + 2, EXTRA = MW + TW + 3;
 };
 
@@ -53,7 +53,7 @@ struct LocalDev {
   const uint32_t* grp_extra;      // [E][MW]
   uint32_t T, R, G, m;
   uint32_t qmin0, qmin1;       // LocalFlat::qmin: |X| below it => empty fixpoint
-  uint32_t scc_mask[8];        // the searched SCC (all m local vertices)
+  uint32_t scc_mask[32];       // the searched SCC (all m local vertices, m <= 1024)
 };
 
 // Wave-uniform tables are read through the constant address space so the compiler emits
@@ -227,10 +227,15 @@ template <int MW>
 struct RecLayout {
   static constexpr int WORDS = MW + 5;
 };
-// witness: key[MW], depth, dlen, q1[MW], order bytes
+// bytes per vertex index in order lists: 1 up to 256 local vertices, 2 beyond
+template <int MW>
+struct OrdBytes {
+  static constexpr int VB = MW > 8 ? 2 : 1;
+};
+// witness: key[MW], depth, dlen, q1[MW], D order (OrdBytes<MW>::VB bytes per entry)
 template <int MW>
 struct WitLayout {
-  static constexpr int ORDW = (UnitLayout<MW>::DMAX + 3) / 4;
+  static constexpr int ORDW = (UnitLayout<MW>::DMAX * OrdBytes<MW>::VB + 3) / 4;
   static constexpr int WORDS = 2 * MW + 2 + ORDW;
 };
 

@@ -272,11 +272,13 @@ def test_ordered_kernel_tiny_budgets(cfg):
         _cmp(qa.FBAS(text).solve_stats(grow, run, blocks), Oracle().load(text).solve(), f"org_t0_{seed}")
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("name", ["tiered_4", "tiered_5", "tiered_5_shuffled", "broken", "correct", "planted_4_64",
                                   "planted_5_96", "two_tier_7_256"])
-def test_ordered_kernel_on_monotone_goldens(name, monkeypatch):
-    # QI_ORDERED=1 forces the order-exact kernel where Jacobi would do: same counts
-    monkeypatch.setenv("QI_ORDERED", "1")
+def test_ordered_kernel_on_monotone_goldens(name, mode, monkeypatch):
+    # QI_ORDERED=1 forces the order-exact kernel (Jacobi fixpoints, as for SCCs beyond
+    # 256 vertices), =2 with the exact Gauss-Seidel sweeps of threshold-0 SCCs: same counts
+    monkeypatch.setenv("QI_ORDERED", mode)
     _cmp(qa.FBAS(_text_for(name)).solve_stats(), GOLD[name], name)
 
 
@@ -582,3 +584,31 @@ def test_cli_sharded_engines_match_oracle(monkeypatch):
         assert timing["engines"] == 3 and timing["stdin_to_verdict_ms"] > 0
     r = subprocess.run([exe], input=fixture_text("correct"), capture_output=True, env=dict(os.environ, QI_DEVICES="0,31"))
     assert r.returncode == 3 and b"no HIP device 31" in r.stderr  # a missing device fails loudly
+
+
+# ---- beyond the Jacobi kernel's shapes: |SCC| > 256 (order-exact kernel, 16-bit lists) ----
+@pytest.mark.parametrize("k,n", [(90, 280), (150, 460)])
+def test_large_scc_beyond_256(k, n):
+    text = fbas_gen.planted(k, n)
+    r = Oracle().load(text).solve()
+    assert len(r["front"]) > 256
+    d = qa.FBAS(text).solve_stats()
+    _cmp(d, r, f"planted_{k}_{n}")
+    _validate_witness(text, d["q1"], d["q2"])
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_gfp_batch_global_scratch(seed, monkeypatch):
+    # networks whose per-query image exceeds the LDS run the batched kernel on global
+    # scratch (QI_GFP_LDS=0 forces that path here)
+    monkeypatch.setenv("QI_GFP_LDS", "0")
+    text = random_fbas(seed, n=30) if seed % 2 else random_org_fbas(seed, 8, t0=True)
+    f, g = qa.FBAS(text), Oracle().load(text)
+    rng = random.Random(seed)
+    nodes = random_masks(rng, f.n, 64, rng.uniform(0.3, 0.95))
+    avail = [sorted(set(s) | {v for v in range(f.n) if rng.random() < 0.2}) for s in nodes]
+    out = qa.sets_from_masks(f.gfp_batch(qa.masks_from_sets(nodes, f.n), qa.masks_from_sets(avail, f.n)), f.n)
+    for s, a, o in zip(nodes, avail, out):
+        av = [v in set(a) for v in range(f.n)]
+        assert sorted(g.contains_quorum(s, av)) == o
+    assert qa.FBAS(text).solve_stats()["verdict"] == g.solve()["verdict"]

@@ -209,8 +209,8 @@ def test_hash_iteration_order_matches_libstdcxx(seed):
     L, P = _oracle_lib(), qa.lib()
     rng = random.Random(seed)
     for trial in range(60):
-        n = rng.choice([1, 2, 5, 13, 14, 15, 29, 30, 31, 59, 60, 61, 127, 128, 129, 200, 256])
-        keys = rng.sample(range(rng.choice([n, 2 * n + 7, 600, 100000])), n)
+        n = rng.choice([1, 2, 5, 13, 14, 15, 29, 30, 31, 59, 60, 61, 127, 128, 129, 200, 256, 257, 258, 300, 541, 542, 700])
+        keys = rng.sample(range(max(n, rng.choice([n, 2 * n + 7, 600, 100000]))), n)
         seq = [rng.randrange(n) for _ in range(rng.randint(0, 2 * n))]
         if rng.random() < 0.5:
             seq = rng.sample(range(n), rng.randint(0, n))
