@@ -38,6 +38,14 @@
 #include "qi_jit.h"
 #include "../../include/quorum_intersection.h"
 
+// The Makefile compiles this file in parts (-DQI_PART=0..4) so the kernel instantiations
+// build in parallel: part 0 holds everything except the search engines, parts 1-4 one group
+// of SearchDeviceImpl instantiations each (make_engine below).  Without QI_PART the file is
+// one translation unit.
+#ifndef QI_PART
+#define QI_PART -1
+#endif
+
 namespace qi {
 
 #define HIP_CHECK(x)                                                                        \
@@ -68,7 +76,7 @@ __global__ __launch_bounds__(64) void ordered_kernel(OrdArgs oa) {
 }
 
 // Fold a host-known best witness into the device-side one (1-word keys).
-__global__ void min_best_kernel(unsigned long long* best64, unsigned long long v) {
+static __global__ void min_best_kernel(unsigned long long* best64, unsigned long long v) {
   if (threadIdx.x == 0) atomicMin(best64, v);
 }
 
@@ -88,11 +96,11 @@ __global__ void gather_units_kernel(const uint32_t* in, uint64_t offset, uint64_
 }
 
 // frontier sort helpers (SearchDeviceImpl::sort_frontier)
-__global__ void iota_kernel(uint32_t* p, uint64_t n) {
+static __global__ void iota_kernel(uint32_t* p, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = (uint32_t)i;
 }
-__global__ void unit_word_kernel(const uint32_t* units, uint32_t words, uint32_t off, const uint32_t* perm, uint64_t n,
+static __global__ void unit_word_kernel(const uint32_t* units, uint32_t words, uint32_t off, const uint32_t* perm, uint64_t n,
                                  uint32_t* keys) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     keys[i] = units[(uint64_t)perm[i] * words + off];
@@ -270,6 +278,7 @@ __global__ __launch_bounds__(64) void gfp_batch_kernel(GlobalDev g, const unsign
 // =====================================================================================
 // Host-side device management
 // =====================================================================================
+#if QI_PART <= 0
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -331,6 +340,7 @@ bool enable_peer(int a, int b) {
   HIP_CHECK(hipSetDevice(prev));
   return true;
 }
+#endif  // QI_PART <= 0
 
 namespace {
 
@@ -1265,8 +1275,39 @@ class SearchDeviceImpl : public SearchDevice {
   uint32_t* gstack_ = nullptr;
 };
 
+size_t GfpDeviceImpl::kLdsImage = 160 * 1024;
+
 }  // namespace
 
+// One search engine shape; explicitly instantiated by the part that owns its group.
+template <int MW, int TW, int SMAX, bool ORD>
+std::unique_ptr<SearchDevice> make_engine(int device, const LocalFlat& f, const SearchConfig& cfg) {
+  return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<MW, TW, SMAX, ORD>(device, f, cfg));
+}
+#define QI_ENGINES_1(X) X(1, 1, 24, false) X(1, 2, 24, false) X(1, 4, 24, false) X(2, 2, 16, false) X(2, 4, 16, false)
+#define QI_ENGINES_2(X) X(4, 4, 12, false) X(4, 8, 12, false) X(8, 8, 8, false)
+#define QI_ENGINES_3(X) X(1, 1, 24, true) X(1, 4, 24, true) X(2, 4, 16, true) X(4, 8, 12, true)
+#define QI_ENGINES_4(X) X(8, 8, 8, true) X(16, 16, 8, true) X(32, 32, 8, true)
+#define QI_ENGINE_DEF(MW, TW, S, O) \
+  template std::unique_ptr<SearchDevice> make_engine<MW, TW, S, O>(int, const LocalFlat&, const SearchConfig&);
+#define QI_ENGINE_EXT(MW, TW, S, O) \
+  extern template std::unique_ptr<SearchDevice> make_engine<MW, TW, S, O>(int, const LocalFlat&, const SearchConfig&);
+#if QI_PART == 0
+QI_ENGINES_1(QI_ENGINE_EXT)
+QI_ENGINES_2(QI_ENGINE_EXT)
+QI_ENGINES_3(QI_ENGINE_EXT)
+QI_ENGINES_4(QI_ENGINE_EXT)
+#elif QI_PART == 1
+QI_ENGINES_1(QI_ENGINE_DEF)
+#elif QI_PART == 2
+QI_ENGINES_2(QI_ENGINE_DEF)
+#elif QI_PART == 3
+QI_ENGINES_3(QI_ENGINE_DEF)
+#elif QI_PART == 4
+QI_ENGINES_4(QI_ENGINE_DEF)
+#endif
+
+#if QI_PART <= 0
 // The ordered kernel's emulation of libstdc++ unordered_set iteration order, run on the
 // host (tests compare it with the real container): keys[v] = global index of local
 // vertex v; the table is built by inserting seq[0..n_seq) in order (repeats ignored).
@@ -1293,7 +1334,6 @@ uint32_t hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint3
   return n;
 }
 
-size_t GfpDeviceImpl::kLdsImage = 160 * 1024;
 
 std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g) {
   if (const char* e = std::getenv("QI_GFP_LDS")) GfpDeviceImpl::kLdsImage = (size_t)std::atoll(e);
@@ -1317,7 +1357,6 @@ bool jit_precompile(const LocalFlat& f, std::string* log) {
 }
 
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg) {
-  using P = std::unique_ptr<SearchDevice>;
   const uint32_t mw = f.mw, tw = f.tw;
   // threshold-0 quorum sets: the order-exact kernel (QI_ORDERED=1 forces it, diagnostics);
   // |SCC| or the TN count beyond 256: the order-exact kernel too (exact for monotone SCCs
@@ -1325,23 +1364,25 @@ std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f,
   const char* fo = std::getenv("QI_ORDERED");
   const bool ordered = f.nonmonotone || (fo && std::atoi(fo) != 0) || mw > 8 || tw > 8;
   if (ordered) {
-    if (mw <= 1 && tw <= 1) return P(new SearchDeviceImpl<1, 1, 24, true>(device, f, cfg));
-    if (mw <= 1 && tw <= 4) return P(new SearchDeviceImpl<1, 4, 24, true>(device, f, cfg));
-    if (mw <= 2 && tw <= 4) return P(new SearchDeviceImpl<2, 4, 16, true>(device, f, cfg));
-    if (mw <= 4 && tw <= 8) return P(new SearchDeviceImpl<4, 8, 12, true>(device, f, cfg));
-    if (mw <= 8 && tw <= 8) return P(new SearchDeviceImpl<8, 8, 8, true>(device, f, cfg));
-    if (mw <= 16 && tw <= 16) return P(new SearchDeviceImpl<16, 16, 8, true>(device, f, cfg));
-    if (mw <= 32 && tw <= 32) return P(new SearchDeviceImpl<32, 32, 8, true>(device, f, cfg));
+    if (mw <= 1 && tw <= 1) return make_engine<1, 1, 24, true>(device, f, cfg);
+    if (mw <= 1 && tw <= 4) return make_engine<1, 4, 24, true>(device, f, cfg);
+    if (mw <= 2 && tw <= 4) return make_engine<2, 4, 16, true>(device, f, cfg);
+    if (mw <= 4 && tw <= 8) return make_engine<4, 8, 12, true>(device, f, cfg);
+    if (mw <= 8 && tw <= 8) return make_engine<8, 8, 8, true>(device, f, cfg);
+    if (mw <= 16 && tw <= 16) return make_engine<16, 16, 8, true>(device, f, cfg);
+    if (mw <= 32 && tw <= 32) return make_engine<32, 32, 8, true>(device, f, cfg);
     throw Error(QI_ERR_UNSUPPORTED, "searched SCC too large for the device kernels (|SCC| > 1024 or > 1024 TNs)");
   }
-  if (mw <= 1 && tw <= 1) return P(new SearchDeviceImpl<1, 1, 24>(device, f, cfg));
-  if (mw <= 1 && tw <= 2) return P(new SearchDeviceImpl<1, 2, 24>(device, f, cfg));
-  if (mw <= 1 && tw <= 4) return P(new SearchDeviceImpl<1, 4, 24>(device, f, cfg));
-  if (mw <= 2 && tw <= 2) return P(new SearchDeviceImpl<2, 2, 16>(device, f, cfg));
-  if (mw <= 2 && tw <= 4) return P(new SearchDeviceImpl<2, 4, 16>(device, f, cfg));
-  if (mw <= 4 && tw <= 4) return P(new SearchDeviceImpl<4, 4, 12>(device, f, cfg));
-  if (mw <= 4 && tw <= 8) return P(new SearchDeviceImpl<4, 8, 12>(device, f, cfg));
-  return P(new SearchDeviceImpl<8, 8, 8>(device, f, cfg));
+  if (mw <= 1 && tw <= 1) return make_engine<1, 1, 24, false>(device, f, cfg);
+  if (mw <= 1 && tw <= 2) return make_engine<1, 2, 24, false>(device, f, cfg);
+  if (mw <= 1 && tw <= 4) return make_engine<1, 4, 24, false>(device, f, cfg);
+  if (mw <= 2 && tw <= 2) return make_engine<2, 2, 16, false>(device, f, cfg);
+  if (mw <= 2 && tw <= 4) return make_engine<2, 4, 16, false>(device, f, cfg);
+  if (mw <= 4 && tw <= 4) return make_engine<4, 4, 12, false>(device, f, cfg);
+  if (mw <= 4 && tw <= 8) return make_engine<4, 8, 12, false>(device, f, cfg);
+  return make_engine<8, 8, 8, false>(device, f, cfg);
 }
+
+#endif  // QI_PART <= 0
 
 }  // namespace qi
