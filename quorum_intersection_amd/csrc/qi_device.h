@@ -43,6 +43,13 @@ struct SearchConfig {
                                  // 0 = off: measured 4.6 vs 4.0 ms per search with 16 (QI_STEAL)
   uint32_t coop_batch = 1;       // parked quorum leaves per cooperative phase (QI_COOP_BATCH; 1 = every
                                  // iteration with a leaf runs the phase)
+  // Persistent full launches (QI_DONATE): the first launch with the run budget runs until
+  // its units are finished, idle lanes taking subtrees busy lanes donate through a queue
+  // in HBM (no grace spills, no relaunch chain).  dq_cap = 0: sized from the unit bytes.
+  uint32_t donate = 0;
+  uint32_t dq_cap = 0;
+  uint32_t dq_margin = 1024;     // ready units kept queued beyond the waiting claims
+  uint32_t dq_shift = 7;         // a polling wave donates ceil(deficit / 2^dq_shift) entries
   uint32_t batch = 0;            // max chained launches per step() (0 = 64)
   uint32_t lookahead = 2;        // launches kept in flight beyond the one the host waits for
   bool keep_log = true;          // keep per-segment records for preorder-exact counts

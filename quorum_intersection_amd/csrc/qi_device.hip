@@ -533,6 +533,18 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_FULL_AT")) cfg_.full_at = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
     if (const char* e = std::getenv("QI_COOP_BATCH")) cfg_.coop_batch = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_DONATE")) cfg_.donate = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_DQ_CAP")) cfg_.dq_cap = (uint32_t)std::atoll(e);
+    if (const char* e = std::getenv("QI_DQ_MARGIN")) cfg_.dq_margin = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_DQ_SHIFT")) cfg_.dq_shift = (uint32_t)std::min(20, std::atoi(e));
+    if (ORD) cfg_.donate = 0;  // the ordered kernel keeps the relaunch chain
+    if (cfg_.donate) {
+      cfg_.steal_max = 0;  // queue slots are the only extra segments of a persistent launch
+      if (!cfg_.dq_cap)    // ~512 MB of queued units, at least 1 M slots
+        cfg_.dq_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((512ull << 20) / UL::BYTES, 1u << 20), 1u << 26);
+      // 32-bit buffer offsets into the queue
+      cfg_.dq_cap = (uint32_t)std::min<uint64_t>(cfg_.dq_cap, 0x7FFFFFF0ull / UL::BYTES);
+    }
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
     if (ORD) cfg_.jit = 1;  // no run-time specialisation of the ordered kernel
@@ -649,7 +661,7 @@ class SearchDeviceImpl : public SearchDevice {
       // auto / cache-only: a specialised kernel already in the on-disk cache runs from the
       // first launch (hipModuleLoadData, ~1 ms); auto compiles a missing one in the
       // background once the search proves long (step()), cache-only never compiles
-      jit_code_ = jit_cached(jit_source(flat_, MW, TW, jit_smax_, false, jit_gstack()));
+      jit_code_ = jit_cached(jit_source(flat_, MW, TW, jit_smax_, false, jit_gstack(), cfg_.donate != 0));
       if (!jit_code_.empty()) {
         jit_state_.store(2);
         load_jit();
@@ -682,6 +694,8 @@ class SearchDeviceImpl : public SearchDevice {
     (void)hipFree(wit_);
     for (auto* p : {sk_[0], sk_[1], sp_[0], sp_[1]}) (void)hipFree(p);
     (void)hipFree(stemp_);
+    (void)hipFree(dq_units_);
+    (void)hipFree(dq_flag_);
     (void)hipEventDestroy(e0_);
     (void)hipEventDestroy(e1_);
     release_stream(device_, stream_);
@@ -734,10 +748,15 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t K = std::max(1u, std::min(cfg_.batch ? cfg_.batch : (uint32_t)kMaxBatch, (uint32_t)kMaxBatch));
     // growing to a target: no look-ahead, so the chain stops at the first launch past it
     const uint32_t D = until ? 0u : std::max(1u, cfg_.lookahead);
-    auto log_need = [&](uint64_t n) {  // the device's log check: n unit records + steals
+    auto log_need = [&](uint64_t n) {  // the device's log check: n unit records + steals / queue slots
       const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
-      return n + nb * 64u * (cfg_.steal_max + 1u);
+      return n + std::max<uint64_t>(nb * 64u * (cfg_.steal_max + 1u), cfg_.donate ? cfg_.dq_cap : 0u);
     };
+    if (cfg_.donate && !dq_units_) {
+      dq_units_ = dalloc<uint32_t>((size_t)cfg_.dq_cap * UL::WORDS);
+      dq_flag_ = dalloc<uint32_t>(cfg_.dq_cap);
+      HIP_CHECK(hipMemsetAsync(dq_flag_, 0, (size_t)cfg_.dq_cap * 4, stream_));
+    }
     auto first_need = [&](uint64_t n) {
       const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
       return n + nb * 64u * (dev::spill_reserve(smax) + cfg_.evict_max);  // search_body's need_out
@@ -787,6 +806,12 @@ class SearchDeviceImpl : public SearchDevice {
     }
     a.gstack = gstack_;
     a.coop_batch = std::max(1u, cfg_.coop_batch);
+    a.donate = spec ? cfg_.donate : 0u;  // the persistent code is in the specialised kernel only
+    a.dq_cap = cfg_.dq_cap;
+    a.dq_margin = cfg_.dq_margin;
+    a.dq_shift = cfg_.dq_shift;
+    a.dq_units = dq_units_;
+    a.dq_flag = dq_flag_;
     a.has_best = has_best_ ? 1u : 0u;
     a.best_depth = best_depth_;
     for (int w = 0; w < 8; ++w) a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
@@ -803,6 +828,8 @@ class SearchDeviceImpl : public SearchDevice {
       a.prev = ctr_ + (size_t)k * dev::CTR_WORDS;
       a.counters = ctr_ + (size_t)(k + 1) * dev::CTR_WORDS;
       a.host_ctr = hctr_dev_ + (size_t)k * dev::HC_WORDS;
+      a.epoch = ++epoch_;  // queue slots published by this launch carry its tag
+      if (a.epoch == 0) a.epoch = ++epoch_;
       if constexpr (ORD) {
         dev::OrdArgs oa = ord_;
         oa.a = a;
@@ -832,6 +859,7 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t g_wit = glob_host_[0], g_flags = glob_host_[1];
     if (g_flags & dev::FLAG_OUT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "search frontier buffer overflow");
     if (g_flags & dev::FLAG_WIT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "witness buffer overflow");
+    if (g_flags & dev::FLAG_DQ_TIMEOUT) throw Error(QI_ERR_STATE, "persistent launch: waves idle past the limit");
     if (g_flags & dev::FLAG_DEPTH)  // zero-fallback steps that keep T (cpp:221, 343): the
       // reference's recursion would not terminate either
       throw Error(QI_ERR_STATE, "search path deeper than the path key (non-terminating recursion)");
@@ -895,6 +923,12 @@ class SearchDeviceImpl : public SearchDevice {
       HIP_CHECK(hipMemcpyAsync(glob_ + 1, &zero, 4, hipMemcpyHostToDevice, stream_));
       HIP_CHECK(hipStreamSynchronize(stream_));
       ++pool_growths_;
+    }
+    if (g_flags & dev::FLAG_DQ_CARRY) {  // a persistent launch left queued units unclaimed
+      const uint32_t keep = g_flags & ~dev::FLAG_DQ_CARRY;
+      HIP_CHECK(hipMemcpyAsync(glob_ + 1, &keep, 4, hipMemcpyHostToDevice, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      ++dq_carries_;
     }
     // The last launch that ran had to carry units over: its lanes spent their node budgets
     // with units left, so launches no longer cover the frontier.  Serve it in preorder
@@ -1200,6 +1234,10 @@ class SearchDeviceImpl : public SearchDevice {
   uint64_t n_ = 0;
   uint32_t idle_steps_ = 0;    // consecutive steps without progress (guard)
   uint64_t max_frontier_bytes_ = 16ull << 30;  // both frontier buffers (QI_MAX_FRONTIER_GB)
+  uint32_t* dq_units_ = nullptr;  // donation queue of persistent launches (cfg_.donate)
+  uint32_t* dq_flag_ = nullptr;
+  uint32_t epoch_ = 0;
+  uint64_t dq_carries_ = 0;
   uint64_t pool_growths_ = 0;  // buffer doublings after a dry eviction pool
   static constexpr uint32_t kMaxBatch = 64;
   uint32_t* ctr_ = nullptr;       // [kMaxBatch + 1][CTR_WORDS]: seed block + one per launch
@@ -1241,7 +1279,7 @@ class SearchDeviceImpl : public SearchDevice {
 
   void start_jit() {
     jit_state_.store(1);
-    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3, jit_gstack());
+    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3, jit_gstack(), cfg_.donate != 0);
     jit_thread_ = std::thread([this, src]() {
       std::vector<char> code = jit_compile(src, &jit_log_);
       jit_code_ = std::move(code);
@@ -1353,7 +1391,8 @@ bool jit_precompile(const LocalFlat& f, std::string* log) {
   else if (mw <= 8 && tw <= 8) { MW = 8; TW = 8; SMAX = 8; }
   else return false;
   if (!jit_eligible(f)) return false;
-  return !jit_compile(jit_source(f, MW, TW, SMAX, false, jit_gstack()), log).empty();
+  const char* dn = std::getenv("QI_DONATE");  // the variant engines created with QI_DONATE load
+  return !jit_compile(jit_source(f, MW, TW, SMAX, false, jit_gstack(), dn && std::atoi(dn) != 0), log).empty();
 }
 
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg) {

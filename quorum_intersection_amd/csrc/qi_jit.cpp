@@ -71,9 +71,10 @@ bool jit_gstack() {
   return on;
 }
 
-std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps, bool gstack) {
+std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps, bool gstack, bool donate) {
   std::ostringstream o;
   if (stamps) o << "#define QI_STAMPS 1\n";
+  if (donate) o << "#define QI_DONATE_CODE 1\n";  // persistent-launch code (else compiled out)
   if (gstack) o << "#define QI_GSTACK 1\n";
   // diagnostics only (never set for measurements): QI_JIT_DEFINES="A,B=2" adds #defines,
   // e.g. the QI_ABL_* ablations of qi_search_kernel.h that repeat one section
@@ -157,6 +158,14 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   o << "      bool same = true;\n";
   for (int w = 0; w < MW; ++w) o << "      n" << w << " &= X[" << w << "]; same &= (n" << w << " == X[" << w << "]);\n";
   o << "      if (same) return true;\n";
+  // survivors below qmin: the greatest fixpoint inside them is empty (LocalFlat::qmin)
+  o << "#if QI_QMIN_ROUND\n";
+  o << "      { const uint32_t c = __popc(n0)";
+  for (int w = 1; w < MW; ++w) o << " + __popc(n" << w << ")";
+  o << "; const uint32_t q = POL == 0 ? " << f.qmin[0] << "u : (POL == 1 ? " << f.qmin[1] << "u : (pol ? " << f.qmin[1]
+    << "u : " << f.qmin[0] << "u));\n        if (c < q) {";
+  for (int w = 0; w < MW; ++w) o << " X[" << w << "] = 0u;";
+  o << " return false; } }\n#endif\n";
   for (int w = 0; w < MW; ++w) o << "      X[" << w << "] = n" << w << ";\n";
   o << "    }\n  }\n";
   // ---------------- findBestNode ----------------
@@ -205,7 +214,7 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
 std::string cache_path(const std::string& src) {
   char key[32];
   const char* xf = std::getenv("QI_JIT_FLAGS");
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v1|" + (xf ? xf : "")));
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v2|" + (xf ? xf : "")));
   return cache_dir() + "/" + key + ".co";
 }
 
@@ -230,7 +239,10 @@ std::vector<char> jit_compile(const std::string& src, std::string* log) {
     if (log) *log = "hiprtcCreateProgram failed";
     return {};
   }
-  std::vector<std::string> optv = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pragma-once-outside-header"};
+  // the atomic optimizer rewrites every lane-0 atomic into a wave scan with an immediate
+  // wait for its result; the kernel's lane-0 atomics are consumed an iteration later
+  std::vector<std::string> optv = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pragma-once-outside-header",
+                                   "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"};
   if (const char* e = std::getenv("QI_JIT_FLAGS")) {  // diagnostics: extra compiler flags (space separated)
     std::istringstream is(e);
     std::string t;

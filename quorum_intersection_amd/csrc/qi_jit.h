@@ -11,7 +11,8 @@ namespace qi {
 // Whether a generated evaluator stays a reasonable size for this SCC.
 bool jit_eligible(const LocalFlat& f);
 // Full hipRTC source: qi_search_kernel.h + generated SpecEval + extern "C" qi_search_spec.
-std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps = false, bool gstack = false);
+std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps = false, bool gstack = false,
+                       bool donate = false);
 // DFS stack of the specialised kernel in global memory (QI_GSTACK, see qi_search_kernel.h)
 bool jit_gstack();
 // Compile for gfx950 (or read the on-disk cache); empty on failure, log in *log.

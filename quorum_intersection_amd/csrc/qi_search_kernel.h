@@ -24,6 +24,7 @@ namespace qi {
 namespace dev {
 
 constexpr int WAVE = 64;
+typedef uint32_t qi_v4u __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------
 // SCC-local TN table (see LocalFlat in qi_internal.h)
@@ -160,6 +161,19 @@ __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32
       same &= (Xn[w] == X[w]);
     }
     if (same) return true;
+#if defined(QI_QMIN_ROUND) && QI_QMIN_ROUND
+    {  // survivors below qmin: the greatest fixpoint inside them is empty
+      uint32_t c = 0;
+#pragma unroll
+      for (int w = 0; w < MW; ++w) c += __popc(Xn[w]);
+      const uint32_t q = POL == 0 ? f.qmin0 : (POL == 1 ? f.qmin1 : (pol ? f.qmin1 : f.qmin0));
+      if (c < q) {
+#pragma unroll
+        for (int w = 0; w < MW; ++w) X[w] = 0u;
+        return false;
+      }
+    }
+#endif
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = Xn[w];
   }
@@ -259,7 +273,10 @@ enum : int {
   C_HALT = 37,     // 1: this launch carried units over (its lanes ran out of budget with
                    // units left); the rest of the chain does nothing and the host sorts
                    // the frontier into preorder before it goes on
-  CTR_WORDS = 64,
+  // donation queue of a persistent launch (SearchArgs::donate), own 128-B line:
+  C_DQLIVE = 64,   // u64: low 32 = slots reserved by donors (tail), high 32 = units finished
+  C_DQHEAD = 96,   // slot tickets taken by waves (64 per claim), own line          [atomic]
+  CTR_WORDS = 128,
   HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6, HC_WORDS = 8
 };
 // Output capacity per launch: n_in (carried-over units) + per used lane SPILL_RESERVE(S)
@@ -304,9 +321,20 @@ struct SearchArgs {
   uint32_t diag;                 // 0; opaque to the compiler (keeps QI_ABL_* repeats alive)
   uint32_t coop_batch;           // parked quorum leaves that trigger a cooperative phase
   uint32_t* gstack;              // QI_GSTACK builds: [blocks][64 lanes][SMAX][2MW+1] DFS stacks
+  // Persistent launches (donate = 1): a launch with the run budget has no node budget and
+  // no grace spill; once its input is claimed, idle lanes take subtrees that busy lanes
+  // donate through a queue in HBM (the bottom stack entry, like an eviction), and the
+  // launch ends when every unit of it has finished (search_body, "donation queue").
+  uint32_t donate;
+  uint32_t dq_cap;               // queue slots (one log record each, after the n_in records)
+  uint32_t dq_margin;            // ready units kept queued beyond the waiting claims
+  uint32_t dq_shift;             // a polling wave donates ceil(deficit / 2^dq_shift) entries
+  uint32_t epoch;                // this launch's publication tag (unique per launch)
+  uint32_t* dq_units;            // [dq_cap][unit words]
+  uint32_t* dq_flag;             // [dq_cap]: epoch of the launch that published the slot
 };
 
-enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u, FLAG_POOL = 8u };
+enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u, FLAG_POOL = 8u, FLAG_DQ_CARRY = 32u, FLAG_DQ_TIMEOUT = 128u };
 
 // 64-bit preorder summary of a node (path key K, depth d) for the device-side best key:
 // MW == 1: (K0, d) -- exact order; MW > 1: (K0, K1) -- "strictly greater" still implies
@@ -405,6 +433,22 @@ constexpr int search_lds_words() {
   } while (0)
 #endif
 
+// QI_DONATE_CODE: the persistent-launch code, compiled only into specialised kernels built
+// for engines with donation on (its mere presence costs the relaunch kernel ~10 %: A/B r02d).
+// QI_QMIN_ROUND: a qmin test after every fixpoint round (measured 3 % slower: off).
+#ifndef QI_DONATE_CODE
+#define QI_DONATE_CODE 0
+#endif
+#ifndef QI_QMIN_ROUND
+#define QI_QMIN_ROUND 0
+#endif
+// iterations between donation-queue polls of a persistent launch
+#ifndef QI_DQ_POLL_MASK
+#define QI_DQ_POLL_MASK 7
+#endif
+#ifndef QI_DQ_IDLE_MAX
+#define QI_DQ_IDLE_MAX (1u << 23)
+#endif
 #ifndef QI_INSTALL_AGE
 #define QI_INSTALL_AGE 0
 #endif
@@ -480,10 +524,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // evictions share what the final spills and the carried-over units leave of out_cap
   const uint64_t spill_need = (uint64_t)n_in + (uint64_t)nb_used * WAVE * spill_reserve(SMAX);
   const uint32_t evict_pool = spill_need < (uint64_t)a.out_cap ? (uint32_t)((uint64_t)a.out_cap - spill_need) : 0u;
+  const uint32_t budget = launch_budget(a, n_in);
+  // persistent launch: the first one with the run budget (the frontier covers the lanes)
+  const bool dmode = QI_DONATE_CODE && a.donate != 0u && budget == a.run_budget;
   {
     // the final spills, and at least evict_max evictions per used lane
     const uint64_t need_out = spill_need + (uint64_t)nb_used * WAVE * (uint64_t)a.evict_max;
-    const uint64_t need_log = (uint64_t)log_base + n_in + (uint64_t)nb_used * WAVE * (a.steal_max + 1u);
+    const uint64_t need_log = (uint64_t)log_base + n_in +
+                              (dmode ? (uint64_t)a.dq_cap : (uint64_t)nb_used * WAVE * (a.steal_max + 1u));
     const bool stop = need_out > (uint64_t)a.out_cap || need_log > (uint64_t)a.log_cap;
     if (blockIdx.x == 0 && lane == 0) {
       cc[C_NIN] = n_in;
@@ -503,7 +551,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     if (stop || blockIdx.x >= nb_used) return;
   }
   uint32_t* const records = a.records + (size_t)log_base * RL::WORDS;
-  const uint32_t budget = launch_budget(a, n_in);
 #ifdef QI_GSTACK
 #define ST_IDX(lvl, w, ln) ((((ln) * SMAX) + (lvl)) * SE + (w))
 #else
@@ -536,17 +583,50 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint32_t steps = 0, steals = 0;
   bool must_spill = false;  // an eviction found the pool empty: spill at the next iteration
   uint32_t xpool_next = 0, xpool_end = 0;  // wave-uniform: claimed extra log record slots
-  uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
+  uint32_t limit = dmode ? 0xFFFFFFFFu : budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
   bool dry = false;         // wave-uniform: no unit left to claim (head >= n_in)
   uint32_t iter = 0;
   // the next unit of this lane: claimed index + (PREFETCH) its words in registers
   // A unit claimed at the end of iteration i is installed at the start of iteration
   // i + 1 + QI_INSTALL_AGE (diagnostics; 0 measured best).
-  bool fpend = false;
+  // fidx is the unit's log record index: its input index, or n_in + its queue slot (fdq)
+  bool fpend = false, fdq = false;
   uint32_t fidx = 0, fage = 1;
   uint32_t fdat[FW];
 #pragma unroll
   for (int q = 0; q < FW; ++q) fdat[q] = 0;
+  // ---- donation queue state (persistent launches, dmode) ----
+  // donor: the bottom stack entry taken this iteration, written at the next iteration's
+  // start (slot = reserved tail base + rank), published (release, epoch tag) at its end
+  bool don_pend = false, flag_pend = false;
+  uint32_t dT[MW], dD[MW], dK[MW], dpk = 0, don_rank = 0, flag_slot = 0;
+#pragma unroll
+  for (int w = 0; w < MW; ++w) dT[w] = dD[w] = dK[w] = 0;
+  unsigned long long don_old = 0;  // lane 0: the tail reservation's returned value
+  bool don_issued = false;         // wave-uniform: a reservation is in flight
+  // claimant: a wave takes 64 slot tickets per atomic (like the input pool) and hands them
+  // to its idle lanes; a lane's slot tag is loaded when it gets the ticket and tested at
+  // each iteration's end until the donor has published it
+  bool dq_wait = false, dq_gone = false;
+  uint32_t dq_idx = 0, dq_seen = 0, dqh_old = 0;
+  uint32_t dqp_next = 0, dqp_end = 0;  // wave-uniform ticket pool
+  bool dq_req_any = false;             // wave-uniform: a ticket atomic is in flight
+  bool flush_pend = false;             // wave-uniform: a finished-count flush is in flight
+  uint32_t fin_cnt = 0;            // units this lane finished since the last flush
+  unsigned long long live_old = 0; // lane 0: the finished-count flush's returned value
+  uint32_t head_seen = 0, fsum_last = 0;
+  bool live_zero = false, dq_full = false;  // wave-uniform, from the last queue poll
+  uint32_t dq_want = 0;                     // wave-uniform: entries to donate this iteration
+  uint32_t idle_iters = 0;                  // wave-uniform: consecutive iterations without work
+  uint32_t dg_idle = 0, dg_wait = 0, dg_evict = 0, dg_vol = 0, dg_atom = 0;  // diagnostics (wave-uniform)
+  unsigned long long* const live64 = (unsigned long long*)(cc + C_DQLIVE);
+  // Queue units cross CUs and XCDs inside the launch: every store and load of them is
+  // write-through / L1-bypassing (sc1, 16-B buffer ops), the donor wave drains its stores
+  // (vmcnt(0)) before the sc1 tag store, and the claimant loads only after its sc1 tag poll
+  // matched -- no L2 write-back or L1 invalidate (MI355X guide, inter-workgroup hand-offs).
+  const __amdgpu_buffer_rsrc_t dqr =
+      __builtin_amdgcn_make_buffer_rsrc(a.dq_units, 0, (int)min((uint64_t)a.dq_cap * UW * 4u, (uint64_t)0x7FFFFFF0u),
+                                        0x00020000);
   // current segment (one per installed unit)
   bool seg_open = false;
   uint32_t seg_idx = 0, seg_depth = 0, seg_count = 0, seg_evals = 0, seg_minq = 0, seg_zfb = 0;
@@ -571,22 +651,44 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   }
 #endif
 
-  auto load_unit = [&](uint32_t idx) {  // issue the loads (consumed at install)
+  // words of the claimed unit: an input unit, or a queue slot (fdq)
+  auto unit_src = [&]() -> const uint32_t* {
+    return fdq ? a.dq_units + (size_t)(fidx - n_in) * UW : a.units_in + (size_t)fidx * UW;
+  };
+  auto load_unit = [&](uint32_t) {  // issue the loads for fidx/fdq (consumed at install)
     if constexpr (PREFETCH) {
-      const uint4* src = (const uint4*)(a.units_in + (size_t)idx * UW);
+      if (fdq) {
+        const uint32_t off = (fidx - n_in) * (uint32_t)(UW * 4);
 #pragma unroll
-      for (int q = 0; q < UW / 4; ++q) {
-        const uint4 v = src[q];
-        fdat[4 * q + 0] = v.x;
-        fdat[4 * q + 1] = v.y;
-        fdat[4 * q + 2] = v.z;
-        fdat[4 * q + 3] = v.w;
+        for (int q = 0; q < UW / 4; ++q) {
+          const qi_v4u v = __builtin_amdgcn_raw_buffer_load_b128(dqr, (int)(off + 16u * q), 0, 16);
+          fdat[4 * q + 0] = v.x;
+          fdat[4 * q + 1] = v.y;
+          fdat[4 * q + 2] = v.z;
+          fdat[4 * q + 3] = v.w;
+        }
+      } else {
+        const uint4* src = (const uint4*)unit_src();
+#pragma unroll
+        for (int q = 0; q < UW / 4; ++q) {
+          const uint4 v = src[q];
+          fdat[4 * q + 0] = v.x;
+          fdat[4 * q + 1] = v.y;
+          fdat[4 * q + 2] = v.z;
+          fdat[4 * q + 3] = v.w;
+        }
       }
     }
   };
   auto unit_word = [&](int wi) -> uint32_t {  // word wi of the claimed unit
-    if constexpr (PREFETCH) return fdat[wi];
-    else return a.units_in[(size_t)fidx * UW + wi];
+    if constexpr (PREFETCH) {
+      return fdat[wi];
+    } else {
+      if (fdq)
+        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(dqr, (int)((fidx - n_in) * (uint32_t)(UW * 4) + 4u * wi), 0,
+                                                              16);
+      return unit_src()[wi];
+    }
   };
   // the statically assigned first unit of this lane (no atomic)
   if (blockIdx.x * WAVE + lane < n_in) {
@@ -625,6 +727,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     rec[MW + 4] = seg_zfb;
     rec_idx = seg_idx;
     rec_pend = true;
+    ++fin_cnt;  // the unit (input or queued) is finished for this launch
     tot_nodes += seg_count;
     tot_evals += seg_evals;
     tot_minq += seg_minq;
@@ -641,13 +744,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   };
 
   // write one unit (T, D given as masks, order = DOW[0..ol) + optional extra byte)
-  auto write_unit = [&](uint32_t slot, const uint32_t (&UT)[MW], const uint32_t (&UD)[MW], const uint32_t (&UK)[MW],
-                        uint32_t udepth, uint32_t ol, int extra_b) {
-    if (slot >= a.out_cap) {
+  auto write_unit_to = [&](uint32_t* ubase, uint32_t ucap, uint32_t slot, const uint32_t (&UT)[MW],
+                           const uint32_t (&UD)[MW], const uint32_t (&UK)[MW], uint32_t udepth, uint32_t ol,
+                           int extra_b) {
+    if (slot >= ucap) {
       atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
       return;
     }
-    uint32_t* u = a.units_out + (size_t)slot * UW;
+    uint32_t* u = ubase + (size_t)slot * UW;
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
       u[UL::T_ + w] = UT[w];
@@ -665,6 +769,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
       u[UL::ORD + i] = word;
     }
+  };
+  auto write_unit = [&](uint32_t slot, const uint32_t (&UT)[MW], const uint32_t (&UD)[MW], const uint32_t (&UK)[MW],
+                        uint32_t udepth, uint32_t ol, int extra_b) {
+    write_unit_to(a.units_out, a.out_cap, slot, UT, UD, UK, udepth, ol, extra_b);
   };
   // a stack entry (T', D', packed) as a unit: the inclusion child it stands for
   auto write_entry = [&](uint32_t slot, const uint32_t (&ET)[MW], const uint32_t (&ED)[MW], uint32_t pk) {
@@ -749,6 +857,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       const uint32_t r = rank_in(wm);
       if (want && r < avail) {
         fidx = pool_next + r;
+        fdq = false;
         fpend = true;
         fage = 0;
         want = false;
@@ -757,13 +866,143 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       pool_next += min((uint32_t)__popcll(wm), avail);
       wm = __ballot(want);
     }
-    if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
+    if (dmode) {
+      // input claimed: idle lanes take queue tickets from the wave's pool; an empty pool
+      // asks for 64 more (one returning atomic, read at the next iteration's start)
+      if (pool_dead) {
+        const bool w2 = want && !dq_wait && !dq_gone && !live_zero;
+        const uint64_t m2 = __ballot(w2);
+        if (m2) {
+          const uint32_t avail = dqp_end - dqp_next, r = rank_in(m2);
+          if (w2 && r < avail) {
+            dq_idx = dqp_next + r;
+            if (dq_idx >= a.dq_cap) {
+              dq_gone = true;  // past the queue: never filled
+            } else {
+              dq_wait = true;
+              dq_seen = __hip_atomic_load(&a.dq_flag[dq_idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+          dqp_next += min((uint32_t)__popcll(m2), avail);
+          if ((uint32_t)__popcll(m2) > avail && !dq_req_any) {
+            if (lane == 0) dqh_old = atomicAdd(&cc[C_DQHEAD], (uint32_t)WAVE);
+            ++dg_atom;
+            dq_req_any = true;
+          }
+        }
+      }
+    } else if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
       dry = true;
       limit = min(limit, steps + a.grace);
     }
   };
 
+  // Donation queue (dmode), once per iteration at its end: publish the units written at
+  // this iteration's start (release, then the epoch tag), and install-prefetch the queue
+  // slots whose tag has appeared (acquire).  The fence's wait covers stores issued a whole
+  // iteration earlier.  Convergent.
+  auto dq_service = [&]() {
+    const bool rdy = dq_wait && dq_seen == a.epoch;
+    if (__any(flag_pend)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 unit stores have landed
+      if (flag_pend) {
+        __hip_atomic_store(&a.dq_flag[flag_slot], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag_pend = false;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the unit loads below the tag poll
+    if (rdy) {
+      dq_wait = false;
+      fidx = n_in + dq_idx;
+      fdq = true;
+      fpend = true;
+      fage = 0;
+      load_unit(fidx);
+    } else if (dq_wait) {
+      dq_seen = __hip_atomic_load(&a.dq_flag[dq_idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  // take this lane's bottom stack entry (the shallowest: the last of its range in
+  // preorder, like an eviction) for donation; its key and D-order prefix stay valid
+  // until the write at the next iteration's start
+  auto take_bottom = [&]() {
+    const uint32_t pos = spos(0);
+#pragma unroll
+    for (int w = 0; w < MW; ++w) {
+      dT[w] = ST_(pos, w);
+      dD[w] = ST_(pos, MW + w);
+      dK[w] = K[w];
+    }
+    dpk = ST_(pos, 2 * MW);
+    key_prefix_bit<MW>(dK, (dpk >> 8) & 511u);
+    sbase_ = spos(1);
+    --nst;
+    don_pend = true;
+  };
+
   for (;;) {
+    // ---- (0) donation queue (dmode): claims and donations issued last iteration -------
+    if (dmode) {
+      if (dq_req_any) {  // 64 fresh tickets for this wave's idle lanes
+        dq_req_any = false;
+        dqp_next = lane0(dqh_old);
+        dqp_end = dqp_next + (uint32_t)WAVE;
+      }
+      if (don_issued) {  // reserved slots: write the donated units
+        don_issued = false;
+        const uint32_t base = lane0((uint32_t)don_old);
+        bool ovf = false;
+        if (don_pend) {
+          don_pend = false;
+          const uint32_t slot = base + don_rank;
+          if (slot < a.dq_cap) {
+            // the unit in 16-B write-through chunks: T, D, key, depth, |D|, then the D
+            // order (bytes past |D| are don't-care; the entry's own vertex merged in)
+            const uint32_t ol = dpk >> 17, ob = dpk & 255u, osh = 8u * (ol & 3u);
+            auto uw = [&](int i) -> uint32_t {
+              if (i < MW) return dT[i];
+              if (i < 2 * MW) return dD[i - MW];
+              if (i < 3 * MW) return dK[i - 2 * MW];
+              if (i == UL::DEPTH) return ((dpk >> 8) & 511u) + 1u;
+              if (i == UL::DLEN) return ol + 1u;
+              if (i >= UL::ORD && i < UL::ORD + OW) {
+                uint32_t word = DOW_(i - UL::ORD);
+                if ((uint32_t)(i - UL::ORD) == (ol >> 2)) word = (word & ~(0xFFu << osh)) | (ob << osh);
+                return word;
+              }
+              return 0u;
+            };
+            const uint32_t off = slot * (uint32_t)(UW * 4);
+#pragma unroll
+            for (int q = 0; q < UW / 4; ++q) {
+              const qi_v4u v = {uw(4 * q), uw(4 * q + 1), uw(4 * q + 2), uw(4 * q + 3)};
+              __builtin_amdgcn_raw_buffer_store_b128(v, dqr, (int)(off + 16u * q), 0, 16);
+            }
+            flag_pend = true;
+            flag_slot = slot;
+          } else {
+            ovf = true;
+            ++fin_cnt;  // the reserved slot is void; the entry leaves through units_out
+          }
+        }
+        const uint64_t om = __ballot(ovf);
+        if (om) {  // queue full: like an eviction (pool token, else this lane's spill reserve)
+          uint32_t tok = 0;
+          if (lane == 0) tok = atomicAdd(&cc[C_EVX], (uint32_t)__popcll(om));
+          tok = lane0(tok);
+          const bool granted = ovf && tok + rank_in(om) < evict_pool;
+          uint32_t total = 0;
+          const uint32_t slot = reserve<1>(ovf ? 1u : 0u, &cc[C_OUT], total);
+          if (ovf) {
+            write_unit(slot, dT, dD, dK, ((dpk >> 8) & 511u) + 1u, dpk >> 17, (int)(dpk & 255u));
+            if (!granted) {
+              must_spill = true;
+              atomicOr(&a.glob[1], FLAG_POOL);
+            }
+          }
+        }
+      }
+    }
     // ---- (1) lanes without a node: pop the top of stack, else install the next unit ----
     if (!done && !has) {
       if (tvalid) {
@@ -919,7 +1158,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 
     QI_STAMP(0);  // pop / install
     // lanes with nothing left: done (a claimed unit past the budget is spilled below)
-    {  // a lane with nothing left is done once it cannot get a unit or steal any more
+    if (dmode) {  // persistent: idle lanes stay until every unit of the launch has finished
+      if (!has && !tvalid && nst == 0 && !fpend && (live_zero || dq_gone)) done = true;
+    } else {  // a lane with nothing left is done once it cannot get a unit or steal any more
       const bool wave_busy = __any(has || tvalid || nst > 0u);
       if (!has && !tvalid && nst == 0 && !fpend &&
           (steps >= limit || (pool_dead && (!wave_busy || steals >= a.steal_max))))
@@ -931,6 +1172,41 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // to claim anywhere, every lane gets a short grace period and then spills: the next
     // launch spreads the remaining subtrees over all lanes instead of letting a few lanes
     // grind through deep subtrees while the rest idle.
+    // Queue poll (dmode, every QI_DQ_POLL_MASK+1 iterations): flush this wave's finished
+    // count into the live word (returning: a consistent (tail, finished) pair) and read
+    // the claim head, one iteration before the values are used.  Live units = n_in +
+    // tail - finished; zero means nothing is held or queued anywhere, and nothing can be
+    // donated any more.  Waiting claims beyond the tail (+ margin) ask for donations.
+    if (dmode) {
+      if (flush_pend) {
+        flush_pend = false;
+        const uint64_t lv = lane0((uint64_t)live_old);
+        const uint32_t hd = lane0(head_seen);
+        const uint32_t tail = (uint32_t)lv;
+        const uint64_t fin = (lv >> 32) + fsum_last;
+        live_zero = (uint64_t)n_in + tail == fin;
+        dq_full = tail >= a.dq_cap;
+        // tickets not yet backed by a reserved slot (+ margin) ask for donations
+        const int32_t deficit = (int32_t)(hd - tail) + (int32_t)a.dq_margin;
+        dq_want = (deficit > 0 && (dry || pool_dead) && !dq_full)
+                      ? min((uint32_t)WAVE, ((uint32_t)deficit + (1u << a.dq_shift) - 1u) >> a.dq_shift)
+                      : 0u;
+      }
+      const bool waiting = __any(dq_wait || (!has && !tvalid && !fpend && !done));
+      if (((iter + 1u) & (waiting ? (uint32_t)QI_DQ_POLL_MASK : 31u)) == 0u) {
+        flush_pend = true;
+        uint32_t fs = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) fs += (uint32_t)__popcll(__ballot((fin_cnt >> b) & 1u)) << b;
+        fin_cnt = 0;
+        fsum_last = fs;
+        if (lane == 0) {
+          live_old = atomicAdd(live64, (unsigned long long)fs << 32);
+          head_seen = __hip_atomic_load(&cc[C_DQHEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ++dg_atom;
+      }
+    }
 #if QI_POLL_ASYNC
     // the loads are issued one iteration before the poll that reads them, so their latency
     // hides behind that iteration (the values are at most one iteration older)
@@ -957,7 +1233,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       best64 = lane0(b);
       if (!dry && h >= n_in) {
         dry = true;
-        limit = min(limit, steps + a.grace);
+        if (!dmode) limit = min(limit, steps + a.grace);
       }
     }
 
@@ -974,7 +1250,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           if (has) write_unit(slot++, T, D, K, depth, dlen, -1);
           if (tvalid) write_entry(slot++, tT, tD, tpk);
           for (uint32_t i = nst; i > 0; --i) write_lds_entry(slot++, spos(i - 1));
-          if (fpend) write_claimed(slot++);
+          if (fpend) {
+            write_claimed(slot++);
+            ++fin_cnt;  // a claimed unit leaves this launch unprocessed
+          }
           nst = 0;
           tvalid = false;
           fpend = false;
@@ -984,7 +1263,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
     }
-    if (!__any(!done)) break;
+    // (a done lane may still hold a written, unpublished queue unit: publish it first)
+    if (!__any(!done || flag_pend)) break;
 
     QI_STAMP(2);  // spill
     // ---- (4) one search node per active lane (cpp:258-345) ---------------------------
@@ -1062,7 +1342,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     {
       const bool evict = push && tvalid && nst == (uint32_t)SMAX;
       bool forced = false;  // no pool slot: the old top leaves through this lane's spill reserve
-      if (__any(evict)) {
+      if (dmode && !dq_full) {  // persistent: the evicted entry is donated to the queue
+        if (evict) take_bottom();
+        dg_evict += (uint32_t)__popcll(__ballot(evict));
+      } else if (__any(evict)) {
         const uint64_t em = __ballot(evict);
         uint32_t tok = 0;
         if (lane == 0) tok = atomicAdd(&cc[C_EVX], (uint32_t)__popcll(em));
@@ -1106,9 +1389,44 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
+    if (dmode) {
+      // voluntary donations: a poll saw waiting claims (or a short queue); lanes with an
+      // entry below their top give their bottom entry, dq_want per wave
+      if (dq_want) {  // (a lane whose only entry is its top gives that, keeping its node)
+        const bool cand = (nst > 0u || (tvalid && has)) && !don_pend;
+        const uint64_t cm = __ballot(cand);
+        dg_vol += min((uint32_t)__popcll(cm), dq_want);
+        if (cand && rank_in(cm) < dq_want) {
+          if (nst > 0u) {
+            take_bottom();
+          } else {
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+              dT[w] = tT[w];
+              dD[w] = tD[w];
+              dK[w] = K[w];
+            }
+            dpk = tpk;
+            key_prefix_bit<MW>(dK, (dpk >> 8) & 511u);
+            tvalid = false;
+            don_pend = true;
+          }
+        }
+        dq_want = 0;
+      }
+      // one tail reservation per wave for this iteration's donations and evictions
+      const uint64_t dm = __ballot(don_pend);
+      if (dm) {
+        don_rank = rank_in(dm);
+        if (lane == 0) don_old = atomicAdd(live64, (unsigned long long)__popcll(dm));
+        ++dg_atom;
+        don_issued = true;
+      }
+    }
     // records of segments closed so far, then the unit loads of lanes that became free:
     // both in flight during the cooperative phase below (the install waits on vmcnt,
     // which counts stores and loads in issue order)
+    if (dmode) dq_service();  // before the record stores: its drain waits for nothing new
     flush_record();
     claim();
     QI_STAMP(4);  // findBestNode + push
@@ -1232,9 +1550,32 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       flush_record();
       claim();
     }
+    // a persistent wave with no work left waits for donations: yield the issue slots
+    if (dmode) {
+      dg_wait += (uint32_t)__popcll(__ballot(dq_wait));
+      if (!__any(has || tvalid || fpend)) {
+        ++dg_idle;
+        __builtin_amdgcn_s_sleep(2);
+        // safety net: a wave idle this long means the queue protocol is broken (never in
+        // a correct run: lanes holding work donate on demand); fail loudly, do not hang
+        if (++idle_iters > (uint32_t)QI_DQ_IDLE_MAX) {
+          if (lane == 0) atomicOr(&a.glob[1], FLAG_DQ_TIMEOUT);
+          done = true;
+        }
+      } else {
+        idle_iters = 0;
+      }
+    }
     ++fage;
   }
   flush_record();
+  if (dmode) {  // finished units not yet counted, and input units this wave claimed but never took
+    uint32_t fs = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) fs += (uint32_t)__popcll(__ballot((fin_cnt >> b) & 1u)) << b;
+    if (pool_next < pool_end) fs += pool_end - pool_next;
+    if (lane == 0 && fs) atomicAdd(live64, (unsigned long long)fs << 32);
+  }
   for (uint32_t i = xpool_next + lane; i < xpool_end; i += WAVE) {  // unused extra record slots
     uint32_t* r = records + (size_t)(n_in + i) * RL::WORDS;
 #pragma unroll
@@ -1283,6 +1624,16 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     atomicAdd(&tt[5], (unsigned long long)tot_fetched);
     atomicAdd(&tt[6], (unsigned long long)wave_iters);
     atomicAdd(&tt[7], (unsigned long long)coop_phases);
+#if !defined(QI_STAMPS) && QI_DONATE_CODE
+    if (dmode) {  // persistent-launch counters (stamps words; no stamps in this build)
+      atomicAdd(&tt[8], (unsigned long long)dg_idle);     // wave-iterations without work
+      atomicAdd(&tt[9], (unsigned long long)dg_wait);     // lane-iterations waiting on a queue slot
+      atomicAdd(&tt[10], (unsigned long long)dg_evict);   // evictions donated
+      atomicAdd(&tt[11], (unsigned long long)dg_vol);     // voluntary donations
+      atomicAdd(&tt[12], (unsigned long long)dg_atom);    // queue atomics issued by this wave
+      atomicAdd(&tt[13], (unsigned long long)wave_iters); // wave-iterations in persistent launches
+    }
+#endif
 #ifdef QI_STAMPS
     for (int q = 0; q < 6; ++q) atomicAdd(&tt[8 + q], (unsigned long long)stamp_sum[q]);
     atomicAdd(&tt[14], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - wave_t0));  // 100 MHz ticks
@@ -1306,6 +1657,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
       hd = lane0(hd);
       out = lane0(out);
+      const uint32_t lane0_out = out;
       const uint32_t head = (uint32_t)min((uint64_t)static_end + hd, (uint64_t)n_in);
       const uint32_t left = n_in - head;
       for (uint32_t i = lane; i < left; i += WAVE) {
@@ -1321,14 +1673,44 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
       uint32_t xr = 0;
-      if (lane == 0) xr = atomicAdd(&cc[C_XREC], 0u);
-      xr = lane0(xr);
+      if (dmode) {
+        // queue slots: their records follow the n_in unit records; slots nobody claimed
+        // (every lane spilled or gave up first) carry over like never-claimed input
+        uint64_t lv = 0;
+        uint32_t dh = 0;
+        if (lane == 0) {
+          lv = atomicAdd(live64, 0ull);
+          dh = atomicAdd(&cc[C_DQHEAD], 0u);
+        }
+        lv = lane0((uint64_t)lv);
+        dh = lane0(dh);
+        xr = min((uint32_t)lv, a.dq_cap);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other waves' queue units
+        const uint32_t dleft = dh < xr ? xr - dh : 0u;
+        for (uint32_t i = lane; i < dleft; i += WAVE) {
+          uint32_t* r = records + (size_t)(n_in + dh + i) * RL::WORDS;
+          for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
+          const uint32_t dst = out + left + i;
+          if (dst < a.out_cap) {
+            const uint4* s4 = (const uint4*)(a.dq_units + (size_t)(dh + i) * UW);
+            uint4* d4 = (uint4*)(a.units_out + (size_t)dst * UW);
+            for (int q = 0; q < UW / 4; ++q) d4[q] = s4[q];
+          } else {
+            atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
+          }
+        }
+        if (dleft && lane == 0) atomicOr(&a.glob[1], FLAG_DQ_CARRY);
+        out += dleft;
+      } else {
+        if (lane == 0) xr = atomicAdd(&cc[C_XREC], 0u);
+        xr = lane0(xr);
+      }
       if (lane == 0) {
         // never-claimed units: the global queue outlived every lane's node budget
         cc[C_HALT] = left ? 1u : 0u;
         a.host_ctr[HC_HALT] = left ? 1u : 0u;
         out += left;
-        if (left) atomicExch(&cc[C_OUT], out);
+        if (out != lane0_out) atomicExch(&cc[C_OUT], out);
         cc[C_LOGN] = log_base + n_in + xr;
         a.host_ctr[HC_LOGN] = log_base + n_in + xr;
         a.host_ctr[HC_OUT] = out;
