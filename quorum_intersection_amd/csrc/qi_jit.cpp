@@ -94,7 +94,7 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   o << "// generated evaluator: m=" << f.m << " T=" << f.T << " R=" << f.R << " G=" << f.G << "\n";
   o << "struct SpecEval {\n";
   // ---------------- containsQuorum ----------------
-  o << "  template <int POL>\n  static __device__ __forceinline__ bool gfp(const LocalDev&, uint32_t (&X)[" << MW
+  o << "  template <int POL, int QR = 0>\n  static __device__ __forceinline__ bool gfp(const LocalDev&, uint32_t (&X)[" << MW
     << "], uint32_t pol, uint32_t& rounds) {\n    (void)pol;\n";
   // |X| < qmin => empty fixpoint (LocalFlat::qmin), before any round
   o << "    { const uint32_t c = __popc(X[0])";
@@ -159,13 +159,12 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   for (int w = 0; w < MW; ++w) o << "      n" << w << " &= X[" << w << "]; same &= (n" << w << " == X[" << w << "]);\n";
   o << "      if (same) return true;\n";
   // survivors below qmin: the greatest fixpoint inside them is empty (LocalFlat::qmin)
-  o << "#if QI_QMIN_ROUND\n";
-  o << "      { const uint32_t c = __popc(n0)";
+  o << "      if (QR || QI_QMIN_ROUND) { const uint32_t c = __popc(n0)";
   for (int w = 1; w < MW; ++w) o << " + __popc(n" << w << ")";
   o << "; const uint32_t q = POL == 0 ? " << f.qmin[0] << "u : (POL == 1 ? " << f.qmin[1] << "u : (pol ? " << f.qmin[1]
     << "u : " << f.qmin[0] << "u));\n        if (c < q) {";
   for (int w = 0; w < MW; ++w) o << " X[" << w << "] = 0u;";
-  o << " return false; } }\n#endif\n";
+  o << " return false; } }\n";
   for (int w = 0; w < MW; ++w) o << "      X[" << w << "] = n" << w << ";\n";
   o << "    }\n  }\n";
   // ---------------- findBestNode ----------------

@@ -99,7 +99,10 @@ __device__ __forceinline__ uint32_t extra_terms(const LocalDev& f, uint32_t t, c
 //     1 = available (visitor, cpp:354/368), 2 = per-lane `pol` (cooperative phase).
 // Same set as the reference's Gauss-Seidel sweep for monotone slices (every quorum set
 // has threshold >= 1); threshold-0 inputs are flagged nonmonotone by the host.
-template <int MW, int TW, int POL>
+// QR: test |survivors| >= qmin after every round too (the cooperative phase's jobs: with
+// |D| - 1 == qmin one round decides; measured 3 % slower on the main fixpoints, which keep
+// the entry test only unless QI_QMIN_ROUND).
+template <int MW, int TW, int POL, int QR = 0>
 __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32_t pol, uint32_t& rounds) {
   using R = TnRec<MW, TW>;
   {  // a non-empty fixpoint needs >= qmin vertices (LocalFlat::qmin): skip the rounds
@@ -162,7 +165,11 @@ __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32
     }
     if (same) return true;
 #if defined(QI_QMIN_ROUND) && QI_QMIN_ROUND
-    {  // survivors below qmin: the greatest fixpoint inside them is empty
+    if (true) {
+#else
+    if (QR) {
+#endif
+      // survivors below qmin: the greatest fixpoint inside them is empty
       uint32_t c = 0;
 #pragma unroll
       for (int w = 0; w < MW; ++w) c += __popc(Xn[w]);
@@ -173,7 +180,6 @@ __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32
         return false;
       }
     }
-#endif
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = Xn[w];
   }
@@ -212,9 +218,9 @@ __device__ __forceinline__ uint32_t best_node(const LocalDev& f, const uint32_t 
 // specialised evaluator with the same interface is generated per FBAS (qi_jit.cpp).
 template <int MW, int TW>
 struct TableEval {
-  template <int POL>
+  template <int POL, int QR = 0>
   static __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32_t pol, uint32_t& rounds) {
-    return dev::gfp<MW, TW, POL>(f, X, pol, rounds);
+    return dev::gfp<MW, TW, POL, QR>(f, X, pol, rounds);
   }
   static __device__ __forceinline__ uint32_t best(const LocalDev& f, const uint32_t (&Q)[MW], const uint32_t (&D)[MW],
                                                   uint32_t& zero_fallback) {
@@ -274,9 +280,11 @@ enum : int {
                    // units left); the rest of the chain does nothing and the host sorts
                    // the frontier into preorder before it goes on
   // donation queue of a persistent launch (SearchArgs::donate), own 128-B line:
-  C_DQLIVE = 64,   // u64: low 32 = slots reserved by donors (tail), high 32 = units finished
+  C_DQLIVE = 64,   // u64: low 32 = slots reserved by donors (tail)                 [atomic]
   C_DQHEAD = 96,   // slot tickets taken by waves (64 per claim), own line          [atomic]
-  CTR_WORDS = 128,
+  C_DQFIN = 128,   // [16 shards, one 128-B line each]: units finished (no-return adds)
+  DQ_FIN_SHARDS = 16,
+  CTR_WORDS = 128 + 32 * 16,
   HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6, HC_WORDS = 8
 };
 // Output capacity per launch: n_in (carried-over units) + per used lane SPILL_RESERVE(S)
@@ -441,6 +449,16 @@ constexpr int search_lds_words() {
 #endif
 #ifndef QI_QMIN_ROUND
 #define QI_QMIN_ROUND 0
+#endif
+#ifndef QI_EARLY_CLAIM
+#define QI_EARLY_CLAIM 1
+#endif
+#ifndef QI_REC_EARLY
+#define QI_REC_EARLY 0  // measured neutral-to-worse (r02a)
+#endif
+// per-round qmin test in the cooperative phase's fixpoints (QR above)
+#ifndef QI_COOP_QR
+#define QI_COOP_QR 0
 #endif
 // iterations between donation-queue polls of a persistent launch
 #ifndef QI_DQ_POLL_MASK
@@ -611,10 +629,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint32_t dq_idx = 0, dq_seen = 0, dqh_old = 0;
   uint32_t dqp_next = 0, dqp_end = 0;  // wave-uniform ticket pool
   bool dq_req_any = false;             // wave-uniform: a ticket atomic is in flight
-  bool flush_pend = false;             // wave-uniform: a finished-count flush is in flight
+
   uint32_t fin_cnt = 0;            // units this lane finished since the last flush
-  unsigned long long live_old = 0; // lane 0: the finished-count flush's returned value
-  uint32_t head_seen = 0, fsum_last = 0;
+  uint32_t fin_v = 0, tail_v = 0, head_v = 0;  // poll loads (lanes 0-15: finished shards; lane 0)
+  uint32_t fin_sum = 0, poll_phase = 0;          // wave-uniform
   bool live_zero = false, dq_full = false;  // wave-uniform, from the last queue poll
   uint32_t dq_want = 0;                     // wave-uniform: entries to donate this iteration
   uint32_t idle_iters = 0;                  // wave-uniform: consecutive iterations without work
@@ -838,7 +856,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   };
 
   auto claim = [&]() {
-    bool want = !done && !has && !fpend && !tvalid && nst == 0 && steps < limit;
+    // QI_EARLY_CLAIM: a lane whose current node is the last thing it holds claims its next
+    // unit already, so the unit's loads have more than one iteration to land (the install's
+    // vmcnt wait stalled on them: -110 cycles per wave-iteration in the pop/install
+    // section, 3.85 vs 3.96 ms per search, r02a)
+    bool want = !done && (QI_EARLY_CLAIM ? true : !has) && !fpend && !tvalid && nst == 0 && steps < limit;
     uint64_t wm = __ballot(want);
     while (wm) {
       if (pool_next >= pool_end) {
@@ -1156,6 +1178,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
+#if QI_REC_EARLY
+    // records of segments closed so far, stored right after the installs: a whole
+    // iteration before the next install's vmcnt wait (which counts stores too)
+    flush_record();
+#endif
     QI_STAMP(0);  // pop / install
     // lanes with nothing left: done (a claimed unit past the budget is spilled below)
     if (dmode) {  // persistent: idle lanes stay until every unit of the launch has finished
@@ -1178,33 +1205,42 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // tail - finished; zero means nothing is held or queued anywhere, and nothing can be
     // donated any more.  Waiting claims beyond the tail (+ margin) ask for donations.
     if (dmode) {
-      if (flush_pend) {
-        flush_pend = false;
-        const uint64_t lv = lane0((uint64_t)live_old);
-        const uint32_t hd = lane0(head_seen);
-        const uint32_t tail = (uint32_t)lv;
-        const uint64_t fin = (lv >> 32) + fsum_last;
-        live_zero = (uint64_t)n_in + tail == fin;
+      // three phases, one per iteration: (A) flush this wave's finished count into its
+      // shard (no-return add) and load the 16 shards; (B) sum them, then load the tail and
+      // the ticket head; (C) evaluate.  The finished counts are read before the tail, and
+      // both only grow, so live = n_in + tail - finished is never below the true count at
+      // the time of the shard loads: zero means nothing is held or queued anywhere, and
+      // nothing can be donated any more.  Tickets beyond the tail ask for donations.
+      if (poll_phase == 2u) {
+        poll_phase = 0;
+        const uint32_t tail = lane0(tail_v), hd = lane0(head_v);
+        live_zero = (uint64_t)n_in + tail == (uint64_t)fin_sum;
         dq_full = tail >= a.dq_cap;
-        // tickets not yet backed by a reserved slot (+ margin) ask for donations
         const int32_t deficit = (int32_t)(hd - tail) + (int32_t)a.dq_margin;
-        dq_want = (deficit > 0 && (dry || pool_dead) && !dq_full)
-                      ? min((uint32_t)WAVE, ((uint32_t)deficit + (1u << a.dq_shift) - 1u) >> a.dq_shift)
-                      : 0u;
-      }
-      const bool waiting = __any(dq_wait || (!has && !tvalid && !fpend && !done));
-      if (((iter + 1u) & (waiting ? (uint32_t)QI_DQ_POLL_MASK : 31u)) == 0u) {
-        flush_pend = true;
-        uint32_t fs = 0;
+        dq_want = (deficit > 0 && (dry || pool_dead) && !dq_full) ? (uint32_t)WAVE : 0u;
+      } else if (poll_phase == 1u) {
+        poll_phase = 2;
+        uint32_t fsum = 0;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) fs += (uint32_t)__popcll(__ballot((fin_cnt >> b) & 1u)) << b;
-        fin_cnt = 0;
-        fsum_last = fs;
+        for (int l = 0; l < DQ_FIN_SHARDS; ++l) fsum += (uint32_t)__builtin_amdgcn_readlane((int)fin_v, l);
+        fin_sum = fsum;
         if (lane == 0) {
-          live_old = atomicAdd(live64, (unsigned long long)fs << 32);
-          head_seen = __hip_atomic_load(&cc[C_DQHEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tail_v = __hip_atomic_load((uint32_t*)live64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          head_v = __hip_atomic_load(&cc[C_DQHEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        ++dg_atom;
+      } else {
+        const bool waiting = __any(dq_wait || (!has && !tvalid && !fpend && !done));
+        if (((iter + 1u) & (waiting ? (uint32_t)QI_DQ_POLL_MASK : 31u)) == 0u) {
+          poll_phase = 1;
+          uint32_t fs = 0;
+#pragma unroll
+          for (int b = 0; b < 8; ++b) fs += (uint32_t)__popcll(__ballot((fin_cnt >> b) & 1u)) << b;
+          fin_cnt = 0;
+          if (lane == 0 && fs) atomicAdd(&cc[C_DQFIN + 32 * (blockIdx.x & (DQ_FIN_SHARDS - 1))], fs);
+          if (lane < (uint32_t)DQ_FIN_SHARDS)
+            fin_v = __hip_atomic_load(&cc[C_DQFIN + 32 * lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ++dg_atom;
+        }
       }
     }
 #if QI_POLL_ASYNC
@@ -1423,11 +1459,12 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         don_issued = true;
       }
     }
-    // records of segments closed so far, then the unit loads of lanes that became free:
-    // both in flight during the cooperative phase below (the install waits on vmcnt,
-    // which counts stores and loads in issue order)
-    if (dmode) dq_service();  // before the record stores: its drain waits for nothing new
+    // the unit loads of lanes that became free: in flight during the cooperative phase
+    // below (the install waits on vmcnt, which counts stores and loads in issue order)
+    if (dmode) dq_service();
+#if !QI_REC_EARLY
     flush_record();
+#endif
     claim();
     QI_STAMP(4);  // findBestNode + push
     // ---- (5) quorum leaves: isMinimalQuorum + visitor, wave-cooperative --------------
@@ -1511,7 +1548,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             if (EV::template gfp<2>(f, Z, vis ? 1u : 0u, rounds) && a.diag == 0x5EEDu) atomicOr(&a.glob[1], 64u);
           }
 #endif
-          const bool ne = EV::template gfp<2>(f, Y, vis ? 1u : 0u, rounds);
+          const bool ne = EV::template gfp<2, QI_COOP_QR>(f, Y, vis ? 1u : 0u, rounds);
           if (act && !vis && ne) atomicOr(&co_NE[(k >> 5) * WAVE + oi], 1u << (k & 31u));
           if (vis) {
 #pragma unroll
@@ -1547,7 +1584,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     }
     QI_STAMP(5);  // quorum-leaf phase
     if (pm) {  // lanes freed by the cooperative phase
+#if !QI_REC_EARLY
       flush_record();
+#endif
       claim();
     }
     // a persistent wave with no work left waits for donations: yield the issue slots
@@ -1574,7 +1613,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll
     for (int b = 0; b < 8; ++b) fs += (uint32_t)__popcll(__ballot((fin_cnt >> b) & 1u)) << b;
     if (pool_next < pool_end) fs += pool_end - pool_next;
-    if (lane == 0 && fs) atomicAdd(live64, (unsigned long long)fs << 32);
+    if (lane == 0 && fs) atomicAdd(&cc[C_DQFIN + 32 * (blockIdx.x & (DQ_FIN_SHARDS - 1))], fs);
   }
   for (uint32_t i = xpool_next + lane; i < xpool_end; i += WAVE) {  // unused extra record slots
     uint32_t* r = records + (size_t)(n_in + i) * RL::WORDS;

@@ -1,4 +1,4 @@
-# Persistent-launch tuning: queue counters and bench lines for a few settings.
+# Persistent-launch tuning: queue counters for a few settings, then a donate-on bench line.
 set -o pipefail
 O=gpurun_out/r02q
 mkdir -p $O
@@ -7,7 +7,8 @@ p() {  # tag, env...
   env QI_DONATE=1 "$@" timeout -k 10 120 python -u tools/dq_probe.py 3 > $O/dq_$tag.jsonl 2> $O/dq_$tag.err || return 1
   echo "$tag $(tail -n 1 $O/dq_$tag.jsonl)"
 }
-p s7m1024 &&
-p s5m1024 QI_DQ_SHIFT=5 &&
-p s3m0 QI_DQ_SHIFT=3 QI_DQ_MARGIN=0 &&
-p s3m8k QI_DQ_SHIFT=3 QI_DQ_MARGIN=8192
+p m0 QI_DQ_MARGIN=0 &&
+p m1024 &&
+p m8k QI_DQ_MARGIN=8192 &&
+QI_DONATE=1 timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_on.json 2> $O/bench_on.err &&
+python3 -c "import json;d=json.loads(open('$O/bench_on.json').read().strip().splitlines()[-1]);print('bench on',round(d['value']/1e9,2),round(d['ms_per_step'],3),d['golden'][:5])"
