@@ -639,6 +639,10 @@ class SearchDeviceImpl : public SearchDevice {
     shm_ = ORD ? 0 : (size_t)dev::search_lds_words<MW, SMAX>() * 4;
     shm_ = (shm_ + 15) / 16 * 16;
     jit_shm_ = shm_ + (size_t)(jit_smax_ - SMAX) * (2 * MW + 1) * 64 * 4;  // QI_JIT_SMAX (diagnostics)
+    if (!ORD) {  // the specialised kernel's D-order words are sized for this SCC (QI_LDS_OW)
+      const size_t ow_full = (dev::UnitLayout<MW>::DMAX + 3) / 4, owl = std::min<size_t>(jit_lds_ow(flat_), ow_full);
+      jit_shm_ -= (ow_full - owl) * 64 * 4;
+    }
     if (jit_gstack()) jit_shm_ = (size_t)dev::search_lds_words<MW, SMAX, true>() * 4;
     jit_shm_ = (jit_shm_ + 15) / 16 * 16;
     const void* kfn;

@@ -59,6 +59,8 @@ std::string cache_dir() {
 
 }  // namespace
 
+uint32_t jit_lds_ow(const LocalFlat& f) { return (f.m / 2 + 1 + 3) / 4; }
+
 bool jit_eligible(const LocalFlat& f) {
   return f.T <= 1024 && f.G <= 1024 && f.extra_src.size() <= 4096 && f.grp_extra.size() <= 4096 * 8;
 }
@@ -75,6 +77,7 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   std::ostringstream o;
   if (stamps) o << "#define QI_STAMPS 1\n";
   if (donate) o << "#define QI_DONATE_CODE 1\n";  // persistent-launch code (else compiled out)
+  o << "#define QI_LDS_OW " << jit_lds_ow(f) << "\n";  // D-order words per lane: |D| <= m/2 + 1
   if (gstack) o << "#define QI_GSTACK 1\n";
   // diagnostics only (never set for measurements): QI_JIT_DEFINES="A,B=2" adds #defines,
   // e.g. the QI_ABL_* ablations of qi_search_kernel.h that repeat one section

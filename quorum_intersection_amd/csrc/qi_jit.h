@@ -10,6 +10,8 @@ namespace qi {
 
 // Whether a generated evaluator stays a reasonable size for this SCC.
 bool jit_eligible(const LocalFlat& f);
+// LDS words of D order per lane in the specialised kernel (QI_LDS_OW): |D| <= m/2 + 1
+uint32_t jit_lds_ow(const LocalFlat& f);
 // Full hipRTC source: qi_search_kernel.h + generated SpecEval + extern "C" qi_search_spec.
 std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps = false, bool gstack = false,
                        bool donate = false);

@@ -450,6 +450,9 @@ constexpr int search_lds_words() {
 #ifndef QI_QMIN_ROUND
 #define QI_QMIN_ROUND 0
 #endif
+#ifndef QI_LDS_OW
+#define QI_LDS_OW 0
+#endif
 #ifndef QI_EARLY_CLAIM
 #define QI_EARLY_CLAIM 1
 #endif
@@ -504,7 +507,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // stack entry: T' [MW] | D of the inclusion child [MW] | packed (b, depth, |D| before b)
   constexpr int SE = 2 * MW + 1;
   constexpr int RB = (SMAX + 3 < 64) ? 6 : (SMAX + 3 < 128 ? 7 : 8);  // bits of a lane's spill count
-  constexpr int OW = (DMAX + 3) / 4;  // packed D-order words (4 vertex bytes each)
+  // packed D-order words (4 vertex bytes each) per lane in LDS; a specialised kernel sizes
+  // them for its SCC (|D| <= m/2 + 1: QI_LDS_OW), which for m <= 31 frees the 256 B that
+  // take a wave from 7 to 8 resident per CU
+  constexpr int OW = (QI_LDS_OW > 0 && QI_LDS_OW < (DMAX + 3) / 4) ? QI_LDS_OW : (DMAX + 3) / 4;
   // the next unit is loaded into registers one node ahead (small units); large units are
   // loaded when installed
   constexpr bool PREFETCH = UW <= 20;
