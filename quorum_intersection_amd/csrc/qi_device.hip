@@ -638,7 +638,13 @@ class SearchDeviceImpl : public SearchDevice {
     HIP_CHECK(hipStreamSynchronize(stream_));
     shm_ = ORD ? 0 : (size_t)dev::search_lds_words<MW, SMAX>() * 4;
     shm_ = (shm_ + 15) / 16 * 16;
-    jit_shm_ = shm_ + (size_t)(jit_smax_ - SMAX) * (2 * MW + 1) * 64 * 4;  // QI_JIT_SMAX (diagnostics)
+    // QI_JIT_SMAX (diagnostics): LDS bytes per stack level as in search_lds_words
+    {
+      const char* jd = std::getenv("QI_JIT_DEFINES");  // diagnostics: QI_PK16=1 (16-bit packed words)
+      const bool pk16 = MW == 1 && jd && std::strstr(jd, "QI_PK16=1");
+      jit_shm_ = (size_t)jit_smax_ * (pk16 ? (2 * 64 + 32) : (2 * MW + 1) * 64) * 4 +
+                 (shm_ - (size_t)SMAX * (2 * MW + 1) * 64 * 4);
+    }
     if (!ORD) {  // the specialised kernel's D-order words are sized for this SCC (QI_LDS_OW)
       const size_t ow_full = (dev::UnitLayout<MW>::DMAX + 3) / 4, owl = std::min<size_t>(jit_lds_ow(flat_), ow_full);
       jit_shm_ -= (ow_full - owl) * 64 * 4;

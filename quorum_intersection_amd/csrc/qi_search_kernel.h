@@ -18,6 +18,7 @@ using __hip_internal::int32_t;
 using __hip_internal::uint32_t;
 using __hip_internal::uint64_t;
 using __hip_internal::uint8_t;
+using __hip_internal::uint16_t;
 #endif
 
 namespace qi {
@@ -412,9 +413,14 @@ __device__ __forceinline__ uint32_t reserve(uint32_t n, uint32_t* counter, uint3
 // LDS words of one search wavefront (search_body's carve-up below).  QI_GSTACK keeps the
 // DFS stack in global memory instead (L1/L2-resident, per-lane contiguous): the LDS then
 // no longer caps the resident waves per CU (7 at MW = 1), registers do.
+#ifndef QI_PK16
+#define QI_PK16 0  // 16-bit packed stack words: 9 waves/CU but measured 2-3 % slower (r02o)
+#endif
 template <int MW, int SMAX, bool GSTACK = false>
 constexpr int search_lds_words() {
-  return (GSTACK ? 0 : SMAX * (2 * MW + 1) * WAVE)  // DFS stack below the top entry
+  // DFS stack below the top entry: T', D' words + a packed (b, depth, |D|) word, which
+  // fits 16 bits when |SCC| <= 32 (halfword array: 640 B per level instead of 768)
+  return (GSTACK ? 0 : ((MW == 1 && QI_PK16) ? SMAX * (2 * WAVE + WAVE / 2) : SMAX * (2 * MW + 1) * WAVE))
          + 2 * MW * WAVE                        // co_NE, co_VIS
          + (MW + 1) * WAVE                      // co_D, co_OWN
          + ((UnitLayout<MW>::DMAX + 3) / 4) * WAVE;  // D order
@@ -517,11 +523,19 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   constexpr int FW = PREFETCH ? UW : 4;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 #ifdef QI_GSTACK
+  constexpr bool PK16 = false;
+  constexpr int SEW = SE;
   uint32_t* const st = a.gstack + (size_t)blockIdx.x * (SMAX * SE * WAVE);  // [64][SMAX][SE]
+  uint16_t* const stpk = nullptr;
   uint32_t* co_NE = lds;                                        // [MW][64] per pending rank
 #else
-  uint32_t* st = lds;                                          // [SMAX][SE][64]
-  uint32_t* co_NE = st + SMAX * SE * WAVE;                      // [MW][64] per pending rank
+  // |SCC| <= 32: the packed word is 16 bits (b < 32, depth < 64, |D| < 32) in its own
+  // halfword array, T' and D' are SEW = 2 words per level
+  constexpr bool PK16 = MW == 1 && QI_PK16;
+  constexpr int SEW = PK16 ? 2 * MW : SE;
+  uint32_t* st = lds;                                          // [SMAX][SEW][64]
+  uint16_t* const stpk = (uint16_t*)(st + SMAX * SEW * WAVE);   // [SMAX][64] (PK16)
+  uint32_t* co_NE = st + SMAX * SEW * WAVE + (PK16 ? SMAX * WAVE / 2 : 0);  // [MW][64] per pending rank
 #endif
   uint32_t* co_VIS = co_NE + MW * WAVE;                         // [MW][64] per pending rank
   uint32_t* co_D = co_VIS + MW * WAVE;                          // [MW][64] pending owners' D
@@ -578,9 +592,23 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #ifdef QI_GSTACK
 #define ST_IDX(lvl, w, ln) ((((ln) * SMAX) + (lvl)) * SE + (w))
 #else
-#define ST_IDX(lvl, w, ln) (((lvl) * SE + (w)) * WAVE + (ln))
+#define ST_IDX(lvl, w, ln) (((lvl) * SEW + (w)) * WAVE + (ln))
 #endif
 #define ST_(lvl, w) st[ST_IDX(lvl, w, lane)]
+  // packed (b, depth, |D| before b) of stack entry `pos` of lane `ln` (register format:
+  // b | depth << 8 | |D| << 17)
+  auto pk_get = [&](uint32_t pos, uint32_t ln) -> uint32_t {
+    if constexpr (PK16) {
+      const uint32_t h = stpk[pos * WAVE + ln];
+      return (h & 31u) | (((h >> 5) & 63u) << 8) | ((h >> 11) << 17);
+    } else {
+      return st[ST_IDX(pos, 2 * MW, ln)];
+    }
+  };
+  auto pk_set = [&](uint32_t pos, uint32_t v) {
+    if constexpr (PK16) stpk[pos * WAVE + lane] = (uint16_t)((v & 31u) | (((v >> 8) & 63u) << 5) | ((v >> 17) << 11));
+    else st[ST_IDX(pos, 2 * MW, lane)] = v;
+  };
 #define DOW_(w) dow[(w) * WAVE + lane]
   // byte i of this lane's D order (ds_write_b8 into the packed word)
   auto set_ord = [&](uint32_t i, uint32_t v) {
@@ -814,7 +842,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       ET[w] = ST_(pos, w);
       ED[w] = ST_(pos, MW + w);
     }
-    write_entry(slot, ET, ED, ST_(pos, 2 * MW));
+    write_entry(slot, ET, ED, pk_get(pos, lane));
   };
   // a claimed but not installed unit goes back out unchanged, its record zeroed
   auto write_claimed = [&](uint32_t slot) {
@@ -961,7 +989,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       dD[w] = ST_(pos, MW + w);
       dK[w] = K[w];
     }
-    dpk = ST_(pos, 2 * MW);
+    dpk = pk_get(pos, lane);
     key_prefix_bit<MW>(dK, (dpk >> 8) & 511u);
     sbase_ = spos(1);
     --nst;
@@ -1061,7 +1089,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
               tT[w] = ST_(pos, w);
               tD[w] = ST_(pos, MW + w);
             }
-            tpk = ST_(pos, 2 * MW);
+            tpk = pk_get(pos, lane);
           } else {
             tvalid = false;
           }
@@ -1150,7 +1178,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
               D[w] = st[ST_IDX(pos, MW + w, dl)];
               K[w] = co_D[w * WAVE + ri];
             }
-            const uint32_t pk = st[ST_IDX(pos, 2 * MW, dl)];
+            const uint32_t pk = pk_get(pos, dl);
             const uint32_t b = pk & 255u, de = (pk >> 8) & 511u, dle = pk >> 17;
             key_prefix_bit<MW>(K, de);
             depth = de + 1;
@@ -1415,7 +1443,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             ST_(pos, w) = tT[w];
             ST_(pos, MW + w) = tD[w];
           }
-          ST_(pos, 2 * MW) = tpk;
+          pk_set(pos, tpk);
           ++nst;
         }
 #pragma unroll
