@@ -32,6 +32,7 @@ std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g);
 struct SearchConfig {
   uint32_t max_blocks = 0;       // 0 = CUs * 8
   uint32_t grow_budget = 2;      // per-lane node budget while the frontier is small (sweeps: 2 < 4 < 8 < 16 < 48 ms)
+  uint32_t ramp_budget = 0;      // budget while the frontier is below 1/64 of the lanes (0 = grow budget)
   uint32_t run_budget = 4096;    // per-lane node budget once the frontier fills the GPU
   uint32_t grace = 24;           // per-lane steps after the unit queue runs dry (sweep: 16-48 best, 64+ worse)
   uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output; 8 stalls deep

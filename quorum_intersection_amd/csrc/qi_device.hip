@@ -534,6 +534,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
     if (const char* e = std::getenv("QI_COOP_BATCH")) cfg_.coop_batch = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_DONATE")) cfg_.donate = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_RAMP_BUDGET")) cfg_.ramp_budget = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_DQ_CAP")) cfg_.dq_cap = (uint32_t)std::atoll(e);
     if (const char* e = std::getenv("QI_DQ_MARGIN")) cfg_.dq_margin = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_DQ_SHIFT")) cfg_.dq_shift = (uint32_t)std::min(20, std::atoi(e));
@@ -797,6 +798,7 @@ class SearchDeviceImpl : public SearchDevice {
     a.totals = totals_;
     a.best64 = best64_;
     a.grow_budget = cfg_.grow_budget;
+    a.ramp_budget = cfg_.ramp_budget;
     a.run_budget = cfg_.run_budget;
     a.grace = cfg_.grace;
     a.steal_max = cfg_.steal_max;

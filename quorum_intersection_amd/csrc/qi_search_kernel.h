@@ -314,6 +314,7 @@ struct SearchArgs {
   unsigned long long* best64;    // device-side best witness, best_pack(): exact when MW == 1,
                                  // the first 64 path bits (conservative pruning) otherwise
   uint32_t grow_budget;          // per-lane node budget while the frontier is below half the lanes
+  uint32_t ramp_budget;          // budget while the frontier is below 1/64 of the lanes (0: grow budget)
   uint32_t run_budget;
   uint32_t grace;                // extra steps per lane once the unit queue is dry
   uint32_t steal_max;            // stacked entries a lane may take from busy lanes per launch
@@ -386,6 +387,9 @@ __device__ __forceinline__ void key_prefix_bit(uint32_t (&K)[MW], uint32_t de) {
 __device__ __forceinline__ uint32_t launch_budget(const SearchArgs& a, uint32_t n_in) {
   const uint64_t lanes8 = (uint64_t)gridDim.x * WAVE;
   const uint64_t n8 = (uint64_t)n_in * 8u;
+  // a tiny frontier (the first launches from the root) digs deeper per lane, so each launch
+  // multiplies the frontier by more than the grow budget's ~3
+  if (a.ramp_budget && (uint64_t)n_in * 64u < lanes8 / 8u) return a.ramp_budget;
   if (n8 < lanes8 * a.run_at) return a.grow_budget;
   if (a.mid_budget && n8 < lanes8 * a.full_at) return a.mid_budget;
   return a.run_budget;

@@ -567,7 +567,10 @@ def test_persistent_launch_bench_workloads_exact(monkeypatch):
              "planted_deep_8_512": fbas_gen.planted_deep(8, 512)}
     for name, text in texts.items():
         d = qa.FBAS(text).solve_stats(jit=2)
-        _cmp(d, BIG[name], name)
+        g = BIG[name]
+        assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (g["verdict"], g["nodes"], g["evals"], g["minq"]), name
+        if "q1" in g:
+            assert (d["q1"], d["q2"]) == (g["q1"], g["q2"]), name
 
 
 # ---- sharded search inside the library (qi_solve_opts.engines / device_mask) ---------------
