@@ -198,6 +198,126 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
       << " bestdeg = better ? deg : bestdeg; bestv = better ? low : bestv; }\n";
   }
   o << "    zero_fallback += (bestdeg == 0u) ? 1u : 0u;\n    return bestv;\n  }\n";
+  // ---------------- minimality of |D| = qmin + 1 quorum leaves ----------------
+  // With |D| = qmin + 1 every D \ {v} has qmin vertices, so it holds a quorum iff it is a
+  // fixpoint itself (cpp:188-198 then finds it non-empty).  One removal-sensitivity pass
+  // over the TN DAG (children first) decides all v at once: count c_t(X\{v}) = c_t(X) -
+  // delta_t(v), where delta_t(v) sums v's direct multiplicity in t and the multiplicities of
+  // satisfied children u with v in crit_u; crit_t = { v : delta_t(v) > c_t - thr_t }.
+  // delta is kept as "at least 1 / 2 / 3" bit masks, so the pass is generated only when
+  // no TN can reach delta 4 for any vertex (per-vertex bound over supports).
+  {
+    const uint32_t mw = f.mw, T = f.T;
+    bool ok = !f.nonmonotone && f.qmin[0] > 0 && T <= 128 && mw <= 2;
+    std::vector<std::vector<uint32_t>> supp(T, std::vector<uint32_t>(mw, 0));
+    std::vector<std::vector<uint32_t>> childrefs(T);  // child TN per reference (with multiplicity)
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> vrefs(T);  // (word, mask) per plane
+    for (uint32_t t = 0; t < T && ok; ++t) {
+      if (f.flags[t] & 1u) ok = false;
+      for (uint32_t w = 0; w < mw; ++w)
+        if (f.vmask[(size_t)t * mw + w]) vrefs[t].push_back({w, f.vmask[(size_t)t * mw + w]});
+      for (uint32_t w = 0; w < f.tw; ++w)
+        for (uint32_t b = 0; b < 32; ++b)
+          if ((f.cmask[(size_t)t * f.tw + w] >> b) & 1u) childrefs[t].push_back(32 * w + b);
+      for (uint32_t e = f.extra_off[t]; e < f.extra_off[t + 1]; ++e) {
+        const uint32_t src = f.extra_src[e], msk = f.extra_mask[e];
+        if (src < mw) vrefs[t].push_back({src, msk});
+        else
+          for (uint32_t b = 0; b < 32; ++b)
+            if ((msk >> b) & 1u) childrefs[t].push_back(32 * (src - mw) + b);
+      }
+      for (auto& pr : vrefs[t]) supp[t][pr.first] |= pr.second;
+      for (uint32_t u : childrefs[t]) {
+        if (u >= t) ok = false;  // children first
+        else
+          for (uint32_t w = 0; w < mw; ++w) supp[t][w] |= supp[u][w];
+      }
+      for (uint32_t v = 0; v < f.m && ok; ++v) {  // delta bound of vertex v at t
+        const uint32_t w = v >> 5, bit = 1u << (v & 31);
+        uint32_t d = 0;
+        for (auto& pr : vrefs[t])
+          if (pr.first == w && (pr.second & bit)) ++d;
+        for (uint32_t u : childrefs[t])
+          if (supp[u][w] & bit) ++d;
+        if (d > 3) ok = false;
+      }
+    }
+    o << "  static constexpr bool FASTMIN = " << (ok ? "true" : "false") << ";\n";
+    o << "  static __device__ __forceinline__ void min_bad(const LocalDev&, const uint32_t (&X)[" << MW
+      << "], uint32_t (&bad)[" << MW << "]) {\n";
+    for (int w = 0; w < MW; ++w) o << "    bad[" << w << "] = 0u;\n";
+    if (ok) {
+      for (uint32_t w = 0; w < f.tw; ++w) o << "    uint32_t sb" << w << " = 0u;\n";
+      for (uint32_t t = 0; t < T; ++t) {
+        const int32_t th = f.thr[2 * t];
+        o << "    uint32_t cr" << t << "_0 = 0u";
+        for (uint32_t w = 1; w < mw; ++w) o << ", cr" << t << "_" << w << " = 0u";
+        o << ";\n    {\n";
+        // count as in gfp
+        std::vector<std::string> terms;  // the count as in gfp: one popcount per mask word
+        for (auto& pr : vrefs[t]) terms.push_back("__popc(X[" + std::to_string(pr.first) + "] & " + hex(pr.second) + ")");
+        for (uint32_t w = 0; w < f.tw; ++w)
+          if (f.cmask[(size_t)t * f.tw + w]) terms.push_back("__popc(sb" + std::to_string(w) + " & " + hex(f.cmask[(size_t)t * f.tw + w]) + ")");
+        for (uint32_t e = f.extra_off[t]; e < f.extra_off[t + 1]; ++e)
+          if (f.extra_src[e] >= mw)
+            terms.push_back("__popc(sb" + std::to_string(f.extra_src[e] - mw) + " & " + hex(f.extra_mask[e]) + ")");
+        std::string c = terms.empty() ? std::string("0u") : terms[0];
+        for (size_t i = 1; i < terms.size(); ++i) c += " + " + terms[i];
+        o << "      const uint32_t c = " << c << "; (void)c;\n";
+        if (th <= 0) {
+          o << "      sb" << (t / 32) << " |= 1u << " << (t % 32) << "u;\n";  // always satisfied, never critical
+        } else if (th != INT32_MAX) {
+          // branch-free (selects): every lane runs the same straight-line code.  The
+          // "at least 2 / 3" masks are only built as far as this TN's delta bound needs.
+          uint32_t dmax = 0;
+          for (uint32_t v = 0; v < f.m; ++v) {
+            const uint32_t w = v >> 5, bit = 1u << (v & 31);
+            uint32_t d = 0;
+            for (auto& pr : vrefs[t])
+              if (pr.first == w && (pr.second & bit)) ++d;
+            for (uint32_t u : childrefs[t])
+              if (supp[u][w] & bit) ++d;
+            dmax = std::max(dmax, d);
+          }
+          o << "      const bool s_ = c >= " << th << "u;\n      sb" << (t / 32) << " |= (uint32_t)s_ << " << (t % 32) << "u;\n";
+          for (uint32_t w = 0; w < mw; ++w) o << "      uint32_t g1_" << w << " = 0u, g2_" << w << " = 0u, g3_" << w << " = 0u;\n";
+          auto acc = [&](uint32_t w, const std::string& m) {
+            o << "      { const uint32_t m_ = " << m << ";";
+            if (dmax >= 3) o << " g3_" << w << " |= g2_" << w << " & m_;";
+            if (dmax >= 2) o << " g2_" << w << " |= g1_" << w << " & m_;";
+            o << " g1_" << w << " |= m_; }\n";
+          };
+          for (auto& pr : vrefs[t]) acc(pr.first, "X[" + std::to_string(pr.first) + "] & " + hex(pr.second));
+          for (uint32_t u : childrefs[t])
+            for (uint32_t w = 0; w < mw; ++w) acc(w, "cr" + std::to_string(u) + "_" + std::to_string(w));
+          o << "      const uint32_t sl = c - " << th << "u;\n";
+          for (uint32_t w = 0; w < mw; ++w) {
+            o << "      cr" << t << "_" << w << " = s_ ? ((sl == 0u ? g1_" << w << " : ";
+            if (dmax >= 2) o << "sl == 1u ? g2_" << w << " : ";
+            if (dmax >= 3) o << "sl == 2u ? g3_" << w << " : ";
+            o << "0u) & X[" << w << "]) : 0u;\n";
+          }
+        }
+        o << "    }\n";
+      }
+      for (uint32_t r = 0; r < f.R; ++r) {
+        const uint32_t tn = f.root_tn[r];
+        o << "    {  // root " << r << "\n";
+        std::string cnt = "0u";
+        for (uint32_t w = 0; w < mw; ++w) {
+          const uint32_t u = f.root_users[(size_t)r * mw + w];
+          o << "      const uint32_t W" << w << " = X[" << w << "] & " << hex(u) << ";\n";
+          cnt += " + __popc(W" + std::to_string(w) + ")";
+        }
+        o << "      const uint32_t n = " << cnt << ";\n      const bool s = (sb" << (tn / 32) << " >> " << (tn % 32)
+          << "u) & 1u;\n      if (n) {\n";
+        for (uint32_t w = 0; w < mw; ++w)
+          o << "        bad[" << w << "] |= (s ? cr" << tn << "_" << w << " : X[" << w << "]) & ~(n == 1u ? W" << w << " : 0u);\n";
+        o << "      }\n    }\n";
+      }
+    }
+    o << "  }\n";
+  }
   // the SCC mask and qmin as literals (no kernel-argument words held in SGPRs)
   o << "  static __device__ __forceinline__ uint32_t scc_word(const LocalDev&, int w) {\n    return ";
   for (int w = 0; w < MW; ++w) {

@@ -229,6 +229,12 @@ struct TableEval {
   }
   static __device__ __forceinline__ uint32_t scc_word(const LocalDev& f, int w) { return f.scc_mask[w]; }
   static __device__ __forceinline__ uint32_t qmin0(const LocalDev& f) { return f.qmin0; }
+  // the removal-sensitivity pass is generated per SCC only (SpecEval::min_bad)
+  static constexpr bool FASTMIN = false;
+  static __device__ __forceinline__ void min_bad(const LocalDev&, const uint32_t (&)[MW], uint32_t (&bad)[MW]) {
+#pragma unroll
+    for (int w = 0; w < MW; ++w) bad[w] = 0u;
+  }
 };
 
 // ------------------------------------------------------------------------------------
@@ -459,6 +465,17 @@ constexpr int search_lds_words() {
 #endif
 #ifndef QI_QMIN_ROUND
 #define QI_QMIN_ROUND 0
+#endif
+#ifndef QI_POP_SCHED
+#define QI_POP_SCHED 0  // no effect on the emitted waits (the register copy stays)
+#endif
+// removal-sensitivity minimality for |D| = qmin + 1 leaves (EV::FASTMIN)
+#ifndef QI_FASTMIN
+#define QI_FASTMIN 1
+#endif
+// QI_COOP_LDS 1: the round-1 cooperative phase (owner slots and results through LDS)
+#ifndef QI_COOP_LDS
+#define QI_COOP_LDS 1  // the cross-lane form measured 3.82-3.85 vs 3.68 ms (r02c)
 #endif
 #ifndef QI_LDS_OW
 #define QI_LDS_OW 0
@@ -1085,6 +1102,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           dlen = dle + 1;
           depth = de + 1;
           has = true;
+#if QI_POP_SCHED
+          // the refill loads go straight into the top registers (already copied out): no
+          // register copy at the join, whose lgkmcnt(0) wait would stall every pop
+          __builtin_amdgcn_sched_barrier(0);
+#endif
           if (nst > 0) {  // refill the top from LDS; first used at the next pop
             --nst;
             const uint32_t pos = spos(nst);
@@ -1533,11 +1555,73 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
     }
+#if QI_FASTMIN
+    // Quorum leaves with |D| = qmin + 1: every D \ {v} has qmin vertices, so it holds a
+    // quorum iff it is a fixpoint itself, which one removal-sensitivity pass decides for
+    // all v at once (EV::min_bad: the v whose removal unsatisfies some remaining member).
+    // isMinimal's first hit (cpp:188-198) is the first D-order position of a v not in bad;
+    // none means D is minimal, and only then does the visitor's fixpoint run (cpp:368).
+    // Credited evals as in the cooperative phase.  No cooperative phase for these leaves.
+    if constexpr (EV::FASTMIN) {
+      const bool fm = pending && dlen == EV::qmin0(f) + 1u;
+      if (__any(fm)) {
+        uint32_t Xd[MW], bad[MW];
+#pragma unroll
+        for (int w = 0; w < MW; ++w) Xd[w] = fm ? D[w] : 0u;
+        EV::min_bad(f, Xd, bad);
+        bool minimal = false;
+        if (fm) {
+          uint32_t ow[OW];
+#pragma unroll
+          for (int i = 0; i < OW; ++i) ow[i] = DOW_(i);
+          uint32_t goodpos = 0;  // bit i: the i-th vertex of the D order is removable
+          if constexpr (MW == 1) {
+            const uint32_t good = ~bad[0];
+#pragma unroll
+            for (int i = 0; i < OW * 4; ++i)  // v_bfe + v_lshrrev + v_and + v_lshl_or per position
+              goodpos |= ((good >> ((ow[i >> 2] >> (8 * (i & 3))) & 31u)) & 1u) << i;
+          } else {
+#pragma unroll
+            for (int i = 0; i < OW * 4; ++i) {
+              const uint32_t v = (ow[i >> 2] >> (8 * (i & 3))) & 255u;
+              uint32_t bw = bad[0];
+#pragma unroll
+              for (int w = 1; w < MW; ++w) bw = (v >> 5) == (uint32_t)w ? bad[w] : bw;
+              goodpos |= (((bw >> (v & 31u)) & 1u) ^ 1u) << i;
+            }
+          }
+          goodpos &= dlen >= 32u ? 0xFFFFFFFFu : ((1u << dlen) - 1u);
+          if (goodpos) {  // not minimal: isMinimal stops at the first removable vertex
+            seg_evals += 2u + (uint32_t)__builtin_ctz(goodpos);  // cpp:184 + (pos+1) x cpp:192
+            has = false;
+            pending = false;
+          } else {
+            minimal = true;
+          }
+        }
+        if (__any(minimal)) {
+          uint32_t Y[MW];
+          uint32_t vany = 0;
+#pragma unroll
+          for (int w = 0; w < MW; ++w) Y[w] = minimal ? (EV::scc_word(f, w) & ~D[w]) : 0u;
+          EV::template gfp<1>(f, Y, 1u, rounds);  // visitor: scc \ Q, outside available
+#pragma unroll
+          for (int w = 0; w < MW; ++w) vany |= Y[w];
+          if (minimal) {
+            has = false;
+            pending = false;
+            minimal_quorum(Y, vany != 0u);
+          }
+        }
+      }
+    }
+#endif
     // Quorum leaves park until coop_batch of them are waiting (one phase then serves up
     // to 64 / S owners per pass) or no lane of the wave has a node left to search.
     park = park || pending;
     const uint64_t pk_m = __ballot(park);
     const uint64_t pm = (pk_m && ((uint32_t)__popcll(pk_m) >= a.coop_batch || !__any(has && !park))) ? pk_m : 0ull;
+#if QI_COOP_LDS
     if (pm) {
       ++coop_phases;
       const uint32_t npend = (uint32_t)__popcll(pm);
@@ -1620,6 +1704,112 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
       QI_COOP_SYNC();
     }
+#else
+    // Cross-lane form of the same phase: the owners of a pass are the next P pending lanes in
+    // lane order (their rank order); every lane reads its group owner's D and |D| with
+    // readlanes (SGPR values, no LDS round trip), only the removed vertex comes from the
+    // owner's D-order bytes in LDS; each chunk's results are one ballot, from which every
+    // owner shifts out its own S bits, and the visitor's survivors reach the owner with one
+    // lane permute.
+    if (pm) {
+      ++coop_phases;
+      const uint32_t npend = (uint32_t)__popcll(pm);
+      const uint32_t r = rank_in(pm);
+      const uint32_t S = a.coop_slot, lgS = a.coop_slot_log2;
+      const uint32_t P = (uint32_t)WAVE >> lgS;  // owners per pass
+      const uint32_t grp = lane >> lgS;          // this lane's slot group
+      const uint64_t maskS = S >= 64u ? ~0ull : ((1ull << S) - 1ull);
+      uint32_t NE[MW], VIS[MW];
+#pragma unroll
+      for (int w = 0; w < MW; ++w) NE[w] = VIS[w] = 0u;
+      uint64_t rem = pm;  // wave-uniform: pending lanes not yet served
+      for (uint32_t q0 = 0; q0 < npend; q0 += P) {
+        uint32_t ol = 0, dl = 0;
+        bool gv = false;  // this lane's group has an owner in this pass
+        uint32_t Dr[MW];
+#pragma unroll
+        for (int w = 0; w < MW; ++w) Dr[w] = 0u;
+        for (uint32_t gi = 0; gi < P && rem; ++gi) {
+          const uint32_t o = (uint32_t)__builtin_ctzll(rem);
+          rem &= rem - 1ull;
+          const uint32_t odl = (uint32_t)__builtin_amdgcn_readlane((int)dlen, (int)o);
+          const bool mine = grp == gi;
+          ol = mine ? o : ol;
+          dl = mine ? odl : dl;
+          gv = gv || mine;
+#pragma unroll
+          for (int w = 0; w < MW; ++w) {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)D[w], (int)o);
+            Dr[w] = mine ? x : Dr[w];
+          }
+        }
+        const bool own = park && r >= q0 && r < q0 + P;  // an owner served in this pass
+        const uint32_t og = r - q0;                       // its group (when own)
+        for (uint32_t c0 = 0; c0 <= a.half_m; c0 += S) {  // jobs 0..|D| (|D| <= half_m)
+          const uint32_t k = c0 + (lane & (S - 1u));
+          const bool act = gv && k <= dl;
+          const bool vis = act && k == dl;
+          // job k < |D| removes the k-th vertex of the owner's D order (its LDS bytes);
+          // NE is indexed by that position, so isMinimal's first hit is one ctz
+          uint32_t v = 0;
+          if (act && !vis) v = (dow[(k >> 2) * WAVE + ol] >> (8u * (k & 3u))) & 255u;
+          uint32_t Y[MW];
+#pragma unroll
+          for (int w = 0; w < MW; ++w) {
+            if (!act) Y[w] = 0u;
+            else if (vis) Y[w] = EV::scc_word(f, w) & ~Dr[w];  // visitor: scc \ Q, outside available
+            else Y[w] = Dr[w];
+          }
+          if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
+          const bool ne = EV::template gfp<2, QI_COOP_QR>(f, Y, vis ? 1u : 0u, rounds);
+          const uint64_t M = __ballot(act && !vis && ne);
+          if (own) {  // this owner's jobs c0 .. c0+S-1 are bits [og*S, og*S+S) of M
+            const uint64_t cb = (M >> (og << lgS)) & maskS;
+            if (S <= 32u) {
+              const uint32_t wi = c0 >> 5, bits = (uint32_t)cb << (c0 & 31u);
+#pragma unroll
+              for (int w = 0; w < MW; ++w)
+                if ((uint32_t)w == wi) NE[w] |= bits;
+            } else {
+#pragma unroll
+              for (int w = 0; w < MW; ++w) {
+                if ((uint32_t)w == (c0 >> 5)) NE[w] |= (uint32_t)cb;
+                if ((uint32_t)w == (c0 >> 5) + 1u) NE[w] |= (uint32_t)(cb >> 32);
+              }
+            }
+          }
+          // the visitor's survivors sit in lane og*S + (|D| - c0) of the chunk holding job |D|
+          const bool vin = own && dlen >= c0 && dlen < c0 + S;
+          const int src = vin ? (int)((og << lgS) + (dlen - c0)) : (int)lane;
+#pragma unroll
+          for (int w = 0; w < MW; ++w) {
+            const uint32_t y = (uint32_t)__shfl((int)Y[w], src);
+            if (vin) VIS[w] = y;
+          }
+          if (c0 + S > a.half_m) break;
+        }
+      }
+      if (park) {
+        park = false;
+        uint32_t ne_any = 0, vis_any = 0;
+#pragma unroll
+        for (int w = 0; w < MW; ++w) {
+          ne_any |= NE[w];
+          vis_any |= VIS[w];
+        }
+        has = false;
+        if (!ne_any) {  // minimal quorum (cpp:283-285)
+          minimal_quorum(VIS, vis_any != 0u);
+        } else {  // not minimal: isMinimal stops at the first removable vertex in D order
+          uint32_t pos = 0;
+#pragma unroll
+          for (int w = MW - 1; w >= 0; --w)
+            if (NE[w]) pos = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(NE[w]);
+          seg_evals += 2u + pos;  // cpp:184 + (pos+1) x cpp:192
+        }
+      }
+    }
+#endif
     QI_STAMP(5);  // quorum-leaf phase
     if (pm) {  // lanes freed by the cooperative phase
 #if !QI_REC_EARLY
