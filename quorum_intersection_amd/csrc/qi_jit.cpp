@@ -148,6 +148,20 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
     o << "      { const uint32_t c = " << c << "; (void)c; sb" << (t / 32) << " |= (uint32_t)(" << bit << ") << "
       << (t % 32) << "u; }\n";
   }
+  // one root TN for every vertex of the SCC (a symmetric tier): all of X survives a round or
+  // none does, so the first round decides and there is no loop
+  bool one_root = f.R == 1;
+  for (uint32_t w = 0; w < f.mw && one_root; ++w) {
+    uint32_t all = 0;
+    for (uint32_t v = 32 * w; v < f.m && v < 32 * w + 32; ++v) all |= 1u << (v & 31);
+    one_root = f.root_users[w] == all;
+  }
+  if (one_root) {
+    const uint32_t tn = f.root_tn[0];
+    o << "#if QI_ONE_ROOT\n      { const bool s_ = (sb" << (tn / 32) << " >> " << (tn % 32) << "u) & 1u; if (!s_) {";
+    for (int w = 0; w < MW; ++w) o << " X[" << w << "] = 0u;";
+    o << " } return s_; }\n#endif\n";
+  }
   for (int w = 0; w < MW; ++w) o << "      uint32_t n" << w << " = 0u;\n";
   for (uint32_t r = 0; r < f.R; ++r) {
     const uint32_t tn = f.root_tn[r];

@@ -469,6 +469,10 @@ constexpr int search_lds_words() {
 #ifndef QI_POP_SCHED
 #define QI_POP_SCHED 0  // no effect on the emitted waits (the register copy stays)
 #endif
+// single-round fixpoint when one root TN serves every vertex (generated evaluator)
+#ifndef QI_ONE_ROOT
+#define QI_ONE_ROOT 1
+#endif
 // removal-sensitivity minimality for |D| = qmin + 1 leaves (EV::FASTMIN)
 #ifndef QI_FASTMIN
 #define QI_FASTMIN 1
