@@ -508,8 +508,11 @@ constexpr int search_lds_words() {
 #define QI_INSTALL_AGE 0
 #endif
 // iterations between polls of the global queue head and the device-side best key
+// (round 2: 127; with the faster round-2 kernel, 32 -> 128 iterations measured 3.45-3.59
+// -> 3.20-3.24 ms per search and 1.50 -> 1.37 ms on planted_deep; 256/512/1024 slower,
+// profiles/r02/ab/poll_*)
 #ifndef QI_POLL_MASK
-#define QI_POLL_MASK 31
+#define QI_POLL_MASK 127
 #endif
 // The cooperative phase's LDS hand-offs stay inside one wavefront (blockDim == 64), whose
 // LDS operations complete in issue order: QI_COOP_WAVESYNC orders them with a wave-level
