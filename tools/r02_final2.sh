@@ -3,7 +3,7 @@
 # planted_deep), N=8 rank-share projection, drop-in time-to-verdict, rocprof stats + PMC.
 # Outputs under gpurun_out/r02z/ and gpurun_out/prof_r02c/.
 set -o pipefail
-O=gpurun_out/r02z
+O=gpurun_out/r02d2
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1 &&
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
@@ -13,5 +13,5 @@ timeout -k 10 200 python -u bench.py --steps 20 --warmup 2 --k-top 7 --validator
 timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --workload planted_deep --no-cpu-baseline > $O/bench_planted_deep.json 2> $O/bench_planted_deep.err &&
 timeout -k 10 200 python -u tools/rank_share_probe.py 8 2048 > $O/rank_share8.jsonl 2> $O/rank_share8.err &&
 timeout -k 10 200 bash tools/ttv_cli.sh > $O/ttv_cli.log 2>&1 &&
-bash tools/profile.sh r02c
+bash tools/profile.sh r02d
 rc=$?; tail -n 2 $O/gpu_tests.log; for f in bench_default bench_192_k8 bench_192_k7 bench_planted_deep; do python3 -c "import json;d=json.loads(open('$O/$f.json').read().strip().splitlines()[-1]);print('$f',round(d['value']/1e9,2),round(d['ms_per_step'],3),d.get('golden','')[:5])" || true; done; tail -n 1 $O/rank_share8.jsonl | cut -c1-300; echo "exit $rc"; exit $rc
