@@ -466,12 +466,6 @@ constexpr int search_lds_words() {
 #ifndef QI_QMIN_ROUND
 #define QI_QMIN_ROUND 0
 #endif
-#ifndef QI_LAZY_TOP
-#define QI_LAZY_TOP 0  // measured 3.48-3.51 vs 3.41-3.42 ms (r02l)
-#endif
-#ifndef QI_POP_SCHED
-#define QI_POP_SCHED 0  // no effect on the emitted waits (the register copy stays)
-#endif
 // single-round fixpoint when one root TN serves every vertex (generated evaluator)
 #ifndef QI_ONE_ROOT
 #define QI_ONE_ROOT 1
@@ -489,9 +483,6 @@ constexpr int search_lds_words() {
 #endif
 #ifndef QI_EARLY_CLAIM
 #define QI_EARLY_CLAIM 1
-#endif
-#ifndef QI_REC_EARLY
-#define QI_REC_EARLY 0  // measured neutral-to-worse (r02a)
 #endif
 // per-round qmin test in the cooperative phase's fixpoints (QR above)
 #ifndef QI_COOP_QR
@@ -658,10 +649,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll
   for (int w = 0; w < MW; ++w) tT[w] = tD[w] = 0;
   bool tvalid = false;
-  // QI_LAZY_TOP: after a pop the new top stays in its LDS slot (spos(nst)) until the end of
-  // the iteration (tin); a push in between just keeps it there (no store, no load), and the
-  // deferred load lands a whole iteration before the next pop reads it
-  bool tin = false;
   uint32_t nst = 0, sbase_ = 0;
   auto spos = [&](uint32_t i) -> uint32_t {  // circular stack position of entry i (0 = bottom)
     const uint32_t p = sbase_ + i;
@@ -921,7 +908,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       atomicMin(a.best64, (unsigned long long)best_pack<MW>(K, depth));
       nst = 0;  // everything left in this unit follows the witness in preorder
       tvalid = false;
-      tin = false;
     }
   };
 
@@ -1098,16 +1084,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // ---- (1) lanes without a node: pop the top of stack, else install the next unit ----
     if (!done && !has) {
       if (tvalid) {
-        if (tin) {  // (not reached: the deferred load runs at every iteration's end)
-          const uint32_t pos = spos(nst);
-#pragma unroll
-          for (int w = 0; w < MW; ++w) {
-            tT[w] = ST_(pos, w);
-            tD[w] = ST_(pos, MW + w);
-          }
-          tpk = pk_get(pos, lane);
-          tin = false;
-        }
         const uint32_t b = tpk & 255u, de = (tpk >> 8) & 511u, dle = tpk >> 17;
         uint32_t NK[MW];
 #pragma unroll
@@ -1127,16 +1103,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           dlen = dle + 1;
           depth = de + 1;
           has = true;
-#if QI_POP_SCHED
-          // the refill loads go straight into the top registers (already copied out): no
-          // register copy at the join, whose lgkmcnt(0) wait would stall every pop
-          __builtin_amdgcn_sched_barrier(0);
-#endif
           if (nst > 0) {  // refill the top from LDS; first used at the next pop
             --nst;
-#if QI_LAZY_TOP
-            tin = true;
-#else
             const uint32_t pos = spos(nst);
 #pragma unroll
             for (int w = 0; w < MW; ++w) {
@@ -1144,7 +1112,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
               tD[w] = ST_(pos, MW + w);
             }
             tpk = pk_get(pos, lane);
-#endif
           } else {
             tvalid = false;
           }
@@ -1267,11 +1234,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
-#if QI_REC_EARLY
-    // records of segments closed so far, stored right after the installs: a whole
-    // iteration before the next install's vmcnt wait (which counts stores too)
-    flush_record();
-#endif
     QI_STAMP(0);  // pop / install
     // lanes with nothing left: done (a claimed unit past the budget is spilled below)
     if (dmode) {  // persistent: idle lanes stay until every unit of the launch has finished
@@ -1373,10 +1335,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         uint32_t slot = reserve<RB>(n, &cc[C_OUT], total);
         if (spill) {
           if (has) write_unit(slot++, T, D, K, depth, dlen, -1);
-          if (tvalid) {
-            if (tin) write_lds_entry(slot++, spos(nst));
-            else write_entry(slot++, tT, tD, tpk);
-          }
+          if (tvalid) write_entry(slot++, tT, tD, tpk);
           for (uint32_t i = nst; i > 0; --i) write_lds_entry(slot++, spos(i - 1));
           if (fpend) {
             write_claimed(slot++);
@@ -1384,7 +1343,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           }
           nst = 0;
           tvalid = false;
-          tin = false;
           fpend = false;
           if (seg_open) close_segment();
           has = false;
@@ -1469,7 +1427,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // reservation, convergent), the new entry becomes the top.  Then continue with the
     // exclusion branch (cpp:336): same D, T = T', key bit 0.
     {
-      const bool evict = push && tvalid && !tin && nst == (uint32_t)SMAX;
+      const bool evict = push && tvalid && nst == (uint32_t)SMAX;
       bool forced = false;  // no pool slot: the old top leaves through this lane's spill reserve
       if (dmode && !dq_full) {  // persistent: the evicted entry is donated to the queue
         if (evict) take_bottom();
@@ -1495,10 +1453,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
       if (push) {
-        if (tvalid && tin) {  // the old top never left its LDS slot
-          ++nst;
-          tin = false;
-        } else if (tvalid) {
+        if (tvalid) {
           const uint32_t pos = spos(nst);
 #pragma unroll
           for (int w = 0; w < MW; ++w) {
@@ -1525,7 +1480,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       // voluntary donations: a poll saw waiting claims (or a short queue); lanes with an
       // entry below their top give their bottom entry, dq_want per wave
       if (dq_want) {  // (a lane whose only entry is its top gives that, keeping its node)
-        const bool cand = (nst > 0u || (tvalid && !tin && has)) && !don_pend;
+        const bool cand = (nst > 0u || (tvalid && has)) && !don_pend;
         const uint64_t cm = __ballot(cand);
         dg_vol += min((uint32_t)__popcll(cm), dq_want);
         if (cand && rank_in(cm) < dq_want) {
@@ -1558,9 +1513,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // the unit loads of lanes that became free: in flight during the cooperative phase
     // below (the install waits on vmcnt, which counts stores and loads in issue order)
     if (dmode) dq_service();
-#if !QI_REC_EARLY
     flush_record();
-#endif
     claim();
     QI_STAMP(4);  // findBestNode + push
     // ---- (5) quorum leaves: isMinimalQuorum + visitor, wave-cooperative --------------
@@ -1848,20 +1801,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #endif
     QI_STAMP(5);  // quorum-leaf phase
     if (pm) {  // lanes freed by the cooperative phase
-#if !QI_REC_EARLY
       flush_record();
-#endif
       claim();
-    }
-    if (tin) {  // the deferred refill of the top (QI_LAZY_TOP)
-      const uint32_t pos = spos(nst);
-#pragma unroll
-      for (int w = 0; w < MW; ++w) {
-        tT[w] = ST_(pos, w);
-        tD[w] = ST_(pos, MW + w);
-      }
-      tpk = pk_get(pos, lane);
-      tin = false;
     }
     // a persistent wave with no work left waits for donations: yield the issue slots
     if (dmode) {
