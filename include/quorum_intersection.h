@@ -77,6 +77,22 @@ int qi_fbas_vertex(const qi_fbas* f, uint32_t v, const char** public_key, const 
  * ------------------------------------------------------------------------------- */
 int qi_gfp_batch(qi_fbas* f, const uint64_t* nodes, const uint64_t* avail, uint32_t count, uint64_t* out);
 
+/* The same batched containsQuorum for callers that cannot allocate (code under HIP graph
+ * capture, tight serving loops, harnesses that forbid hipMalloc).  No counterpart in the
+ * reference.  nodes / avail / out are DEVICE memory on the qi_fbas's HIP device, laid out
+ * as for qi_gfp_batch.  The per-query state (available set, candidate set, one byte per
+ * threshold node) and a counter header live in a fixed array of QI_STATIC_SCRATCH_BYTES
+ * that the library holds on every GPU it runs on until the process ends; the call makes no
+ * hipMalloc / hipFree / hipHostMalloc and no other allocating call.  `stream`: a
+ * hipStream_t to enqueue on without synchronising, or NULL to run on the library's stream
+ * and wait.  Set-up is not part of it: the qi_fbas must have run qi_gfp_batch or qi_solve
+ * once (that uploads the threshold-node tables), else QI_ERR_STATE.  count queries whose
+ * state exceeds the array: QI_ERR_CAPACITY (split the batch).  Every call on a GPU uses
+ * that GPU's one array: calls that overlap on one GPU (other threads, other streams) race. */
+#define QI_STATIC_SCRATCH_BYTES (4u << 20)
+int qi_gfp_batch_static(qi_fbas* f, const uint64_t* d_nodes, const uint64_t* d_avail, uint32_t count,
+                        uint64_t* d_out, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * solve(Graph) (cpp:615-707): per-SCC quorum checks (cpp:649-672, batched on the GPU),
  * the "exactly one SCC contains a quorum" rule (cpp:681-688) and the branch-and-bound

@@ -116,6 +116,13 @@ class FBAS:
         check(lib().qi_gfp_batch(self._h, _u64p(nodes), _u64p(avail), nodes.shape[0], _u64p(out)))
         return out
 
+    def gfp_batch_static(self, d_nodes: int, d_avail: int, count: int, d_out: int, stream: int = 0) -> None:
+        """qi_gfp_batch_static: the same fixpoints on DEVICE masks (raw device addresses of
+        [count, ceil(n/64)] uint64 arrays on this FBAS's GPU) with no allocation; needs one
+        earlier gfp_batch / solve on this FBAS (set-up)."""
+        check(lib().qi_gfp_batch_static(self._h, ctypes.c_void_p(d_nodes), ctypes.c_void_p(d_avail), count,
+                                        ctypes.c_void_p(d_out), ctypes.c_void_p(stream or None)))
+
     def containsQuorum(self, nodes: Sequence[int], availableNodes: Sequence[bool]) -> List[int]:
         """containsQuorum(nodes, availableNodes) (cpp:140-177): survivors in `nodes` order."""
         avail_set = [v for v, a in enumerate(availableNodes) if a]

@@ -110,6 +110,7 @@ SIGNATURES = {
     "qi_fbas_adjacency": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
     "qi_fbas_vertex": (c_int, [c_void_p, c_uint32, POINTER(c_char_p), POINTER(c_char_p)]),
     "qi_gfp_batch": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64), c_uint32, POINTER(c_uint64)]),
+    "qi_gfp_batch_static": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p]),
     "qi_solve": (c_int, [c_void_p, POINTER(SolveOpts), POINTER(SolveResult), POINTER(c_uint32), POINTER(c_uint32)]),
     "qi_solve_text": (c_int, [c_void_p, c_int, c_int, POINTER(c_void_p), POINTER(c_int)]),
     "qi_solve_text_ex": (c_int, [c_void_p, c_int, c_int, POINTER(SolveOpts), POINTER(c_void_p), POINTER(c_int)]),

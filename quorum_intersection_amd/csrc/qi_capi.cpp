@@ -200,6 +200,19 @@ int qi_gfp_batch(qi_fbas* f, const uint64_t* nodes, const uint64_t* avail, uint3
   });
 }
 
+int qi_gfp_batch_static(qi_fbas* f, const uint64_t* d_nodes, const uint64_t* d_avail, uint32_t count, uint64_t* d_out,
+                        void* stream) {
+  if (!f || (count && (!d_nodes || !d_avail || !d_out))) return fail(QI_ERR_ARG, "null argument");
+  // set-up (table upload, scratch address) allocates and belongs to an earlier call
+  if (!f->gfp)
+    return fail(QI_ERR_STATE, "qi_gfp_batch_static: no device image yet; call qi_gfp_batch or qi_solve once on this "
+                              "qi_fbas first (set-up allocates, this entry point never does)");
+  return guarded([&] {
+    f->gfp->run_static(d_nodes, d_avail, count, d_out, stream);
+    return QI_OK;
+  });
+}
+
 int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32_t* q1, uint32_t* q2) {
   if (!f || !res) return fail(QI_ERR_ARG, "null argument");
   if (opts && opts->tiebreak != QI_TIE_LOWEST) return fail(QI_ERR_UNSUPPORTED, "only QI_TIE_LOWEST is implemented");

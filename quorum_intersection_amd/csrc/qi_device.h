@@ -18,6 +18,13 @@ class GfpDevice {
   virtual ~GfpDevice() = default;
   // nodes/avail/out: count x words(n) uint64 masks in host memory.
   virtual void run(const uint64_t* nodes, const uint64_t* avail, uint32_t count, uint64_t* out) = 0;
+  // The same fixpoints for callers that cannot allocate: masks in DEVICE memory, per-query
+  // state in the library's fixed device scratch array (QI_STATIC_SCRATCH_BYTES per GPU, shared
+  // by every call on that GPU), no hipMalloc / hipFree / hipHostMalloc.  stream = a
+  // hipStream_t to enqueue on (no synchronisation), or null: the engine's own stream, waited
+  // for before returning.  Throws QI_ERR_CAPACITY when count queries do not fit the array.
+  virtual void run_static(const uint64_t* d_nodes, const uint64_t* d_avail, uint32_t count, uint64_t* d_out,
+                          void* stream) = 0;
   virtual double last_kernel_ms() const = 0;
 };
 std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g);

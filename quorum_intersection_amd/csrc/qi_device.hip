@@ -275,6 +275,47 @@ __global__ __launch_bounds__(64) void gfp_batch_kernel(GlobalDev g, const unsign
 
 }  // namespace dev
 
+#if QI_PART <= 0
+// ------------------------------------------------------------------------------------
+// Device scratch of the no-allocation entry point (GfpDevice::run_static): one fixed array
+// per GPU, held from the first use of the library on that GPU until the process ends.
+//   [0, 256)   counters (fixpoint rounds of the last call), cleared by every call
+//   [256, ...) per-query state images (available set, candidates, TN satisfaction bytes)
+// In host code the array's name is only a handle: the device address is taken once per
+// device with hipGetSymbolAddress (static_scratch_ptr) and only that pointer is passed on.
+// ------------------------------------------------------------------------------------
+namespace dev {
+// Clears `n` 64-bit words (a kernel rather than hipMemsetAsync: callers may be capturing
+// the stream into a HIP graph).
+static __global__ void zero_u64_kernel(unsigned long long* p, uint32_t n) {
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0ull;
+}
+}  // namespace dev
+constexpr size_t kStaticScratchBytes = QI_STATIC_SCRATCH_BYTES;
+constexpr size_t kStaticScratchHeader = 256;
+static __device__ __align__(256) unsigned char scratch[kStaticScratchBytes];
+
+namespace {
+std::mutex g_scratch_mu;
+unsigned char* g_scratch_ptr[64] = {};  // per HIP device: address of that device's copy
+
+// Call with `device` current.  Resolves the array's address on this device (first call per
+// device; a set-up step, done when the device image of an FBAS is created).
+unsigned char* static_scratch_ptr(int device) {
+  if (device < 0 || device >= 64) throw Error(QI_ERR_ARG, "static scratch: device ordinal out of range");
+  std::lock_guard<std::mutex> g(g_scratch_mu);
+  if (!g_scratch_ptr[device]) {
+    unsigned char* p = nullptr;
+    HIP_CHECK(hipGetSymbolAddress((void**)&p, HIP_SYMBOL(scratch)));
+    if (!p) throw Error(QI_ERR_DEVICE, "static scratch: hipGetSymbolAddress returned null");
+    g_scratch_ptr[device] = p;
+  }
+  return g_scratch_ptr[device];
+}
+}  // namespace
+
+#endif  // QI_PART <= 0
+
 // =====================================================================================
 // Host-side device management
 // =====================================================================================
@@ -405,10 +446,12 @@ struct DeviceGuard {
   ~DeviceGuard() { (void)hipSetDevice(prev); }
 };
 
+#if QI_PART <= 0
 class GfpDeviceImpl : public GfpDevice {
  public:
   GfpDeviceImpl(int device, const GlobalFlat& g) : device_(device) {
     DeviceGuard dg(device_);
+    static_ = static_scratch_ptr(device_);  // set-up: this device's scratch array address
     stream_ = acquire_stream(device_);
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
@@ -483,10 +526,43 @@ class GfpDeviceImpl : public GfpDevice {
     HIP_CHECK(hipEventElapsedTime(&ms, e0_, e1_));
     last_ms_ = ms;
   }
+  // No allocation on this path: the tables were uploaded by the constructor, the masks are
+  // the caller's device memory and the per-query state lives in this GPU's static scratch
+  // array.  Every call on a GPU shares that array (calls that overlap on one GPU race) and
+  // finds the previous call's contents in it: the counter header is cleared by a fill
+  // kernel, the state images are fully rewritten by the kernel before it reads them.
+  void run_static(const uint64_t* d_nodes, const uint64_t* d_avail, uint32_t count, uint64_t* d_out,
+                  void* stream) override {
+    if (count == 0) return;
+    DeviceGuard dg(device_);
+    const size_t per = (size_t)d_.words * 16 + ((d_.T + 15) / 16) * 16;  // multiple of 16 B
+    const size_t room = kStaticScratchBytes - kStaticScratchHeader;
+    if (per > room || (size_t)count > room / per)
+      throw Error(QI_ERR_CAPACITY, "qi_gfp_batch_static: " + std::to_string(count) + " queries x " + std::to_string(per) +
+                                       " B of state exceed the " + std::to_string(room) + " B static scratch (at most " +
+                                       std::to_string(room / per) + " queries per call for this network)");
+    for (const void* p : {(const void*)d_nodes, (const void*)d_avail, (const void*)d_out}) {
+      hipPointerAttribute_t at{};
+      if (hipPointerGetAttributes(&at, p) != hipSuccess ||
+          (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeManaged) || at.device != device_) {
+        (void)hipGetLastError();
+        throw Error(QI_ERR_ARG, "qi_gfp_batch_static: masks must be device memory of HIP device " + std::to_string(device_));
+      }
+    }
+    hipStream_t s = stream ? (hipStream_t)stream : stream_;
+    unsigned long long* rounds = (unsigned long long*)static_;
+    hipLaunchKernelGGL(dev::zero_u64_kernel, dim3(1), dim3(64), 0, s, rounds, (uint32_t)(kStaticScratchHeader / 8));
+    hipLaunchKernelGGL(dev::gfp_batch_kernel<true>, dim3(count), dim3(64), 0, s, d_,
+                       (const unsigned long long*)d_nodes, (const unsigned long long*)d_avail, count,
+                       (unsigned long long*)d_out, rounds, (uint8_t*)(static_ + kStaticScratchHeader), per);
+    HIP_CHECK(hipGetLastError());
+    if (!stream) HIP_CHECK(hipStreamSynchronize(stream_));
+  }
   double last_kernel_ms() const override { return last_ms_; }
 
  private:
   int device_;
+  unsigned char* static_ = nullptr;  // this device's static scratch array (device address)
   hipStream_t stream_{};
   hipEvent_t e0_{}, e1_{};
   dev::GlobalDev d_{};
@@ -502,6 +578,8 @@ class GfpDeviceImpl : public GfpDevice {
  private:
   double last_ms_ = 0;
 };
+size_t GfpDeviceImpl::kLdsImage = 160 * 1024;
+#endif  // QI_PART <= 0
 
 // ORD = false: search_kernel / the run-time specialised kernel (monotone SCCs);
 // ORD = true: ordered_kernel (SCCs with threshold-0 quorum sets), same protocol.
@@ -1324,8 +1402,6 @@ class SearchDeviceImpl : public SearchDevice {
   }
   uint32_t* gstack_ = nullptr;
 };
-
-size_t GfpDeviceImpl::kLdsImage = 160 * 1024;
 
 }  // namespace
 
