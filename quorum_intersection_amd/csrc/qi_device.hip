@@ -983,6 +983,9 @@ class SearchDeviceImpl : public SearchDevice {
       float ms = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, ev_[k], ev_[k + 1]));
       ms_sum += ms;
+      if (trace_)
+        std::fprintf(stderr, "[qi]     launch %u: in %u out %u halt %u, %.1f us\n", k, c[dev::HC_NIN], c[dev::HC_OUT],
+                     c[dev::HC_HALT], ms * 1e3);
     }
     n_ = n_next;
     cur_ = cur_next;

@@ -14,6 +14,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -350,14 +351,26 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
 std::string cache_path(const std::string& src) {
   char key[32];
   const char* xf = std::getenv("QI_JIT_FLAGS");
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v2|" + (xf ? xf : "")));
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v3|" + (xf ? xf : "")));
   return cache_dir() + "/" + key + ".co";
 }
 
+// A cache entry is the code object followed by an 16-byte trailer: "QICO" + its length +
+// an FNV-1a hash of its bytes.  A file without a matching trailer (partly written, left by
+// a crashed process, older format) is ignored and overwritten by the next compile.
 std::vector<char> jit_cached(const std::string& src) {
   std::ifstream in(cache_path(src), std::ios::binary);
   if (!in) return {};
-  return std::vector<char>((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+  std::vector<char> buf((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+  if (buf.size() < 16) return {};
+  const size_t n = buf.size() - 16;
+  uint32_t len = 0;
+  uint64_t h = 0;
+  std::memcpy(&len, &buf[n + 4], 4);
+  std::memcpy(&h, &buf[n + 8], 8);
+  if (std::memcmp(&buf[n], "QICO", 4) != 0 || len != n || h != fnv1a(std::string(buf.data(), n))) return {};
+  buf.resize(n);
+  return buf;
 }
 
 std::vector<char> jit_compile(const std::string& src, std::string* log) {
@@ -399,10 +412,17 @@ std::vector<char> jit_compile(const std::string& src, std::string* log) {
     code.resize(cs);
     hiprtcGetCode(prog, code.data());
     ::mkdir(dir.c_str(), 0755);
-    const std::string tmp = path + ".tmp" + std::to_string(::getpid());
+    // unique per process AND thread (sharded solves compile on several threads at once)
+    static std::atomic<uint32_t> seq{0};
+    const std::string tmp = path + ".tmp" + std::to_string(::getpid()) + "." + std::to_string(seq.fetch_add(1));
     {
       std::ofstream out(tmp, std::ios::binary);
       out.write(code.data(), (std::streamsize)code.size());
+      const uint32_t len = (uint32_t)code.size();
+      const uint64_t h = fnv1a(std::string(code.data(), code.size()));
+      out.write("QICO", 4);
+      out.write((const char*)&len, 4);
+      out.write((const char*)&h, 8);
     }
     std::rename(tmp.c_str(), path.c_str());
   }

@@ -309,13 +309,14 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
         if rank == 0:
             be.grow(target)
         n = torch.tensor([be.frontier() if rank == 0 else 0], dtype=torch.int64, device=device)
-        dist.broadcast(n, 0, group=group)
+        # group rank 0 as a global rank (broadcast takes global ranks, also with a sub-group)
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(n, src, group=group)
         n = int(n.item())
         # (2) ... hands it to every rank; each keeps its dealt share (rotating offset)
         if rank != 0:
             be.clear()
         if n:
-            src = dist.get_global_rank(group, 0) if group is not None else 0
             buf = _unit_buf(be, n, device)
             _settle(buf)
             if rank == 0:

@@ -604,6 +604,60 @@ def test_sharded_bench_workloads_exact():
         _cmp(d, g, name)
 
 
+@pytest.mark.parametrize("engines", [2, 4, 8])
+def test_sharded_configs3_workload_exact(engines):
+    # BASELINE configs[3]'s exact workload (the bench's 121 M-node full search) through the
+    # sharded code path, as many engines as the 1/2/4/8-GPU legs use, all on device 0
+    g = BIG["two_tier_10_256"]
+    d = qa.FBAS(fbas_gen.two_tier(10, 256)).solve_stats(engines=engines, device_mask=1, jit=2)
+    assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (g["verdict"], g["nodes"], g["evals"], g["minq"])
+    assert d["engines"] == engines and d["devices"] == 1
+
+
+@pytest.mark.parametrize("engines", [2, 8])
+def test_sharded_planted_deep_exact(engines):
+    # configs[4] (deep early exit) through 2 and 8 engines: preorder-exact counts and the
+    # preorder-first witness whatever engine finds it
+    g = BIG["planted_deep_8_512"]
+    d = qa.FBAS(fbas_gen.planted_deep(8, 512)).solve_stats(engines=engines, device_mask=1, jit=2)
+    _cmp(d, g, "planted_deep_8_512")
+
+
+# ---- one process per rank over the real engine (the code path of bench.py --gpus N) --------
+@pytest.mark.parametrize("name,batch,seed_units", [("two_tier_8_192", 64, 0), ("planted_deep_8_512", 64, 0),
+                                                   ("planted_deep_8_512", 2, 300), ("tiered_6", 1, 64)])
+def test_distributed_search_real_engine_two_ranks(name, batch, seed_units, tmp_path):
+    # distributed_search over DeviceSearch with gloo world_size 2: two fresh child processes
+    # (started before anything in them touches the GPU) share device 0; golden nodes / evals /
+    # minq / witness.  Small batches and seeds force exchanges and send/recv rebalancing.
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "result.json"
+    worker = os.path.join(ROOT, "tests", "dist_rank_worker.py")
+    procs = [subprocess.Popen([sys.executable, "-u", worker, str(r), "2", str(port), name, str(out), str(batch),
+                               str(seed_units)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(2)]
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=200)[0].decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+    d = json.load(open(out))
+    g = BIG[name] if name in BIG else GOLD[name]
+    assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (g["verdict"], g["nodes"], g["evals"] - g["scc_evals"],
+                                                                 g["minq"]), logs
+    if not g["verdict"]:
+        assert (d["q1"], d["q2"]) == (g["q1"], g["q2"])
+
+
 def test_cli_sharded_engines_match_oracle(monkeypatch):
     import subprocess
     exe = os.path.join(ROOT, "bin", "quorum_intersection")
