@@ -39,25 +39,11 @@ std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g);
 struct SearchConfig {
   uint32_t max_blocks = 0;       // 0 = CUs * 8
   uint32_t grow_budget = 2;      // per-lane node budget while the frontier is small (sweeps: 2 < 4 < 8 < 16 < 48 ms)
-  uint32_t ramp_budget = 0;      // budget while the frontier is below 1/64 of the lanes (0 = grow budget)
   uint32_t run_budget = 4096;    // per-lane node budget once the frontier fills the GPU
   uint32_t grace = 24;           // per-lane steps after the unit queue runs dry (sweep: 16-48 best, 64+ worse)
   uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output; 8 stalls deep
                                  // multi-word searches, 8/32/64 equal on the bench)
   uint32_t run_at = 4;           // run budget once the frontier holds >= run_at/8 of the resident lanes
-  uint32_t mid_budget = 0;       // budget between run_at/8 and full_at/8 of the lanes (0 = run budget)
-  uint32_t full_at = 8;
-  uint32_t steal_max = 0;        // per-lane entries taken from busy lanes per launch (bounds the log);
-                                 // 0 = off: measured 4.6 vs 4.0 ms per search with 16 (QI_STEAL)
-  uint32_t coop_batch = 1;       // parked quorum leaves per cooperative phase (QI_COOP_BATCH; 1 = every
-                                 // iteration with a leaf runs the phase)
-  // Persistent full launches (QI_DONATE): the first launch with the run budget runs until
-  // its units are finished, idle lanes taking subtrees busy lanes donate through a queue
-  // in HBM (no grace spills, no relaunch chain).  dq_cap = 0: sized from the unit bytes.
-  uint32_t donate = 0;
-  uint32_t dq_cap = 0;
-  uint32_t dq_margin = 1024;     // ready units kept queued beyond the waiting claims
-  uint32_t dq_shift = 7;         // a polling wave donates ceil(deficit / 2^dq_shift) entries
   uint32_t batch = 0;            // max chained launches per step() (0 = 64)
   uint32_t lookahead = 2;        // launches kept in flight beyond the one the host waits for
   bool keep_log = true;          // keep per-segment records for preorder-exact counts

@@ -605,25 +605,8 @@ class SearchDeviceImpl : public SearchDevice {
     // tuning overrides for experiments (profiling only; defaults are the measured best)
     if (const char* e = std::getenv("QI_GRACE")) cfg_.grace = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("QI_STEAL")) cfg_.steal_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("QI_MID_BUDGET")) cfg_.mid_budget = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("QI_FULL_AT")) cfg_.full_at = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
-    if (const char* e = std::getenv("QI_COOP_BATCH")) cfg_.coop_batch = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("QI_DONATE")) cfg_.donate = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("QI_RAMP_BUDGET")) cfg_.ramp_budget = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("QI_DQ_CAP")) cfg_.dq_cap = (uint32_t)std::atoll(e);
-    if (const char* e = std::getenv("QI_DQ_MARGIN")) cfg_.dq_margin = (uint32_t)std::atoi(e);
-    if (const char* e = std::getenv("QI_DQ_SHIFT")) cfg_.dq_shift = (uint32_t)std::min(20, std::atoi(e));
-    if (ORD) cfg_.donate = 0;  // the ordered kernel keeps the relaunch chain
-    if (cfg_.donate) {
-      cfg_.steal_max = 0;  // queue slots are the only extra segments of a persistent launch
-      if (!cfg_.dq_cap)    // ~512 MB of queued units, at least 1 M slots
-        cfg_.dq_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((512ull << 20) / UL::BYTES, 1u << 20), 1u << 26);
-      // 32-bit buffer offsets into the queue
-      cfg_.dq_cap = (uint32_t)std::min<uint64_t>(cfg_.dq_cap, 0x7FFFFFF0ull / UL::BYTES);
-    }
     jit_smax_ = SMAX;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
     if (ORD) cfg_.jit = 1;  // no run-time specialisation of the ordered kernel
@@ -708,7 +691,7 @@ class SearchDeviceImpl : public SearchDevice {
     totals_ = dalloc<unsigned long long>(16 * dev::TOT_SHARDS);
     best64_ = dalloc<unsigned long long>(1);
     red_ = dalloc<unsigned long long>(4);
-    keydev_ = dalloc<uint32_t>(8);
+    keydev_ = dalloc<uint32_t>(dev::KEY_WORDS_MAX);
     wit_cap_ = 1u << 16;
     wit_ = dalloc<uint32_t>((size_t)wit_cap_ * WL::WORDS);
     HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * dev::TOT_SHARDS * sizeof(unsigned long long), stream_));
@@ -718,17 +701,11 @@ class SearchDeviceImpl : public SearchDevice {
     shm_ = ORD ? 0 : (size_t)dev::search_lds_words<MW, SMAX>() * 4;
     shm_ = (shm_ + 15) / 16 * 16;
     // QI_JIT_SMAX (diagnostics): LDS bytes per stack level as in search_lds_words
-    {
-      const char* jd = std::getenv("QI_JIT_DEFINES");  // diagnostics: QI_PK16=1 (16-bit packed words)
-      const bool pk16 = MW == 1 && jd && std::strstr(jd, "QI_PK16=1");
-      jit_shm_ = (size_t)jit_smax_ * (pk16 ? (2 * 64 + 32) : (2 * MW + 1) * 64) * 4 +
-                 (shm_ - (size_t)SMAX * (2 * MW + 1) * 64 * 4);
-    }
+    jit_shm_ = (size_t)jit_smax_ * (2 * MW + 1) * 64 * 4 + (shm_ - (size_t)SMAX * (2 * MW + 1) * 64 * 4);
     if (!ORD) {  // the specialised kernel's D-order words are sized for this SCC (QI_LDS_OW)
       const size_t ow_full = (dev::UnitLayout<MW>::DMAX + 3) / 4, owl = std::min<size_t>(jit_lds_ow(flat_), ow_full);
       jit_shm_ -= (ow_full - owl) * 64 * 4;
     }
-    if (jit_gstack()) jit_shm_ = (size_t)dev::search_lds_words<MW, SMAX, true>() * 4;
     jit_shm_ = (jit_shm_ + 15) / 16 * 16;
     const void* kfn;
     if constexpr (ORD) kfn = (const void*)dev::ordered_kernel<MW, TW>;
@@ -750,7 +727,7 @@ class SearchDeviceImpl : public SearchDevice {
       // auto / cache-only: a specialised kernel already in the on-disk cache runs from the
       // first launch (hipModuleLoadData, ~1 ms); auto compiles a missing one in the
       // background once the search proves long (step()), cache-only never compiles
-      jit_code_ = jit_cached(jit_source(flat_, MW, TW, jit_smax_, false, jit_gstack(), cfg_.donate != 0));
+      jit_code_ = jit_cached(jit_source(flat_, MW, TW, jit_smax_, false));
       if (!jit_code_.empty()) {
         jit_state_.store(2);
         load_jit();
@@ -783,8 +760,6 @@ class SearchDeviceImpl : public SearchDevice {
     (void)hipFree(wit_);
     for (auto* p : {sk_[0], sk_[1], sp_[0], sp_[1]}) (void)hipFree(p);
     (void)hipFree(stemp_);
-    (void)hipFree(dq_units_);
-    (void)hipFree(dq_flag_);
     (void)hipEventDestroy(e0_);
     (void)hipEventDestroy(e1_);
     release_stream(device_, stream_);
@@ -837,15 +812,7 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t K = std::max(1u, std::min(cfg_.batch ? cfg_.batch : (uint32_t)kMaxBatch, (uint32_t)kMaxBatch));
     // growing to a target: no look-ahead, so the chain stops at the first launch past it
     const uint32_t D = until ? 0u : std::max(1u, cfg_.lookahead);
-    auto log_need = [&](uint64_t n) {  // the device's log check: n unit records + steals / queue slots
-      const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
-      return n + std::max<uint64_t>(nb * 64u * (cfg_.steal_max + 1u), cfg_.donate ? cfg_.dq_cap : 0u);
-    };
-    if (cfg_.donate && !dq_units_) {
-      dq_units_ = dalloc<uint32_t>((size_t)cfg_.dq_cap * UL::WORDS);
-      dq_flag_ = dalloc<uint32_t>(cfg_.dq_cap);
-      HIP_CHECK(hipMemsetAsync(dq_flag_, 0, (size_t)cfg_.dq_cap * 4, stream_));
-    }
+    auto log_need = [&](uint64_t n) { return n; };  // the device's log check: one record per input unit
     auto first_need = [&](uint64_t n) {
       const uint64_t nb = std::min<uint64_t>((n + 63) / 64, blocks);
       return n + nb * 64u * (dev::spill_reserve(smax) + cfg_.evict_max);  // search_body's need_out
@@ -876,13 +843,9 @@ class SearchDeviceImpl : public SearchDevice {
     a.totals = totals_;
     a.best64 = best64_;
     a.grow_budget = cfg_.grow_budget;
-    a.ramp_budget = cfg_.ramp_budget;
     a.run_budget = cfg_.run_budget;
     a.grace = cfg_.grace;
-    a.steal_max = cfg_.steal_max;
     a.run_at = cfg_.run_at;
-    a.mid_budget = cfg_.mid_budget;
-    a.full_at = cfg_.full_at;
     a.evict_max = cfg_.evict_max;
     a.half_m = m_ / 2;
     {  // cooperative slot: smallest power of two covering |D| + 1 <= half_m + 1 jobs
@@ -894,17 +857,10 @@ class SearchDeviceImpl : public SearchDevice {
       a.coop_slot = sl;
       a.coop_slot_log2 = lg;
     }
-    a.gstack = gstack_;
-    a.coop_batch = std::max(1u, cfg_.coop_batch);
-    a.donate = spec ? cfg_.donate : 0u;  // the persistent code is in the specialised kernel only
-    a.dq_cap = cfg_.dq_cap;
-    a.dq_margin = cfg_.dq_margin;
-    a.dq_shift = cfg_.dq_shift;
-    a.dq_units = dq_units_;
-    a.dq_flag = dq_flag_;
     a.has_best = has_best_ ? 1u : 0u;
     a.best_depth = best_depth_;
-    for (int w = 0; w < 8; ++w) a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
+    static_assert(MW <= dev::KEY_WORDS_MAX, "path key wider than the key buffers");
+    for (int w = 0; w < dev::KEY_WORDS_MAX; ++w) a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
     if (MW == 1 && has_best_ && best_dirty_) {  // 1-word keys: the device best is exact; fold the host's in
       hipLaunchKernelGGL(dev::min_best_kernel, dim3(1), dim3(64), 0, stream_, best64_,
                          ((unsigned long long)best_key_[0] << 32) | best_depth_);
@@ -918,8 +874,6 @@ class SearchDeviceImpl : public SearchDevice {
       a.prev = ctr_ + (size_t)k * dev::CTR_WORDS;
       a.counters = ctr_ + (size_t)(k + 1) * dev::CTR_WORDS;
       a.host_ctr = hctr_dev_ + (size_t)k * dev::HC_WORDS;
-      a.epoch = ++epoch_;  // queue slots published by this launch carry its tag
-      if (a.epoch == 0) a.epoch = ++epoch_;
       if constexpr (ORD) {
         dev::OrdArgs oa = ord_;
         oa.a = a;
@@ -949,7 +903,6 @@ class SearchDeviceImpl : public SearchDevice {
     const uint32_t g_wit = glob_host_[0], g_flags = glob_host_[1];
     if (g_flags & dev::FLAG_OUT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "search frontier buffer overflow");
     if (g_flags & dev::FLAG_WIT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "witness buffer overflow");
-    if (g_flags & dev::FLAG_DQ_TIMEOUT) throw Error(QI_ERR_STATE, "persistent launch: waves idle past the limit");
     if (g_flags & dev::FLAG_DEPTH)  // zero-fallback steps that keep T (cpp:221, 343): the
       // reference's recursion would not terminate either
       throw Error(QI_ERR_STATE, "search path deeper than the path key (non-terminating recursion)");
@@ -1016,12 +969,6 @@ class SearchDeviceImpl : public SearchDevice {
       HIP_CHECK(hipMemcpyAsync(glob_ + 1, &zero, 4, hipMemcpyHostToDevice, stream_));
       HIP_CHECK(hipStreamSynchronize(stream_));
       ++pool_growths_;
-    }
-    if (g_flags & dev::FLAG_DQ_CARRY) {  // a persistent launch left queued units unclaimed
-      const uint32_t keep = g_flags & ~dev::FLAG_DQ_CARRY;
-      HIP_CHECK(hipMemcpyAsync(glob_ + 1, &keep, 4, hipMemcpyHostToDevice, stream_));
-      HIP_CHECK(hipStreamSynchronize(stream_));
-      ++dq_carries_;
     }
     // The last launch that ran had to carry units over: its lanes spent their node budgets
     // with units left, so launches no longer cover the frontier.  Serve it in preorder
@@ -1138,9 +1085,10 @@ class SearchDeviceImpl : public SearchDevice {
     // no witness: every segment counts, and the running totals are exactly those sums
     if (!has_key) return running_totals();
     DeviceGuard dg(device_);
-    std::vector<uint32_t> k(8, 0);
-    for (size_t i = 0; i < key.size() && i < 8; ++i) k[i] = key[i];
-    HIP_CHECK(hipMemcpyAsync(keydev_, k.data(), 32, hipMemcpyHostToDevice, stream_));
+    // the whole key (MW words): reduce_kernel compares every word of a record's key
+    std::vector<uint32_t> k(dev::KEY_WORDS_MAX, 0);
+    for (size_t i = 0; i < key.size() && i < (size_t)dev::KEY_WORDS_MAX; ++i) k[i] = key[i];
+    HIP_CHECK(hipMemcpyAsync(keydev_, k.data(), k.size() * 4, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(red_, 0, 32, stream_));
     for (auto& c : log_) {
       if (!c.used) continue;
@@ -1327,10 +1275,6 @@ class SearchDeviceImpl : public SearchDevice {
   uint64_t n_ = 0;
   uint32_t idle_steps_ = 0;    // consecutive steps without progress (guard)
   uint64_t max_frontier_bytes_ = 16ull << 30;  // both frontier buffers (QI_MAX_FRONTIER_GB)
-  uint32_t* dq_units_ = nullptr;  // donation queue of persistent launches (cfg_.donate)
-  uint32_t* dq_flag_ = nullptr;
-  uint32_t epoch_ = 0;
-  uint64_t dq_carries_ = 0;
   uint64_t pool_growths_ = 0;  // buffer doublings after a dry eviction pool
   static constexpr uint32_t kMaxBatch = 64;
   uint32_t* ctr_ = nullptr;       // [kMaxBatch + 1][CTR_WORDS]: seed block + one per launch
@@ -1372,7 +1316,7 @@ class SearchDeviceImpl : public SearchDevice {
 
   void start_jit() {
     jit_state_.store(1);
-    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3, jit_gstack(), cfg_.donate != 0);
+    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3);
     jit_thread_ = std::thread([this, src]() {
       std::vector<char> code = jit_compile(src, &jit_log_);
       jit_code_ = std::move(code);
@@ -1398,12 +1342,7 @@ class SearchDeviceImpl : public SearchDevice {
         max_blocks_ = cus_ * (uint32_t)nb;
       }
     }
-    if (jit_gstack()) {  // one stack region per resident block: [64 lanes][SMAX][2MW+1]
-      const size_t words = (size_t)max_blocks_ * 64u * (size_t)jit_smax_ * (2 * MW + 1);
-      keep(gstack_ = dalloc<uint32_t>(words));
-    }
   }
-  uint32_t* gstack_ = nullptr;
 };
 
 }  // namespace
@@ -1482,8 +1421,7 @@ bool jit_precompile(const LocalFlat& f, std::string* log) {
   else if (mw <= 8 && tw <= 8) { MW = 8; TW = 8; SMAX = 8; }
   else return false;
   if (!jit_eligible(f)) return false;
-  const char* dn = std::getenv("QI_DONATE");  // the variant engines created with QI_DONATE load
-  return !jit_compile(jit_source(f, MW, TW, SMAX, false, jit_gstack(), dn && std::atoi(dn) != 0), log).empty();
+  return !jit_compile(jit_source(f, MW, TW, SMAX, false), log).empty();
 }
 
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg) {

@@ -66,22 +66,12 @@ bool jit_eligible(const LocalFlat& f) {
   return f.T <= 1024 && f.G <= 1024 && f.extra_src.size() <= 4096 && f.grp_extra.size() <= 4096 * 8;
 }
 
-bool jit_gstack() {
-  static const bool on = [] {
-    const char* e = std::getenv("QI_GSTACK");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return on;
-}
-
-std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps, bool gstack, bool donate) {
+std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps) {
   std::ostringstream o;
   if (stamps) o << "#define QI_STAMPS 1\n";
-  if (donate) o << "#define QI_DONATE_CODE 1\n";  // persistent-launch code (else compiled out)
   o << "#define QI_LDS_OW " << jit_lds_ow(f) << "\n";  // D-order words per lane: |D| <= m/2 + 1
-  if (gstack) o << "#define QI_GSTACK 1\n";
-  // diagnostics only (never set for measurements): QI_JIT_DEFINES="A,B=2" adds #defines,
-  // e.g. the QI_ABL_* ablations of qi_search_kernel.h that repeat one section
+  // diagnostics only (never set for measurements): QI_JIT_DEFINES="A,B=2" adds #defines
+  // for A/B runs of the kernel's compile-time switches
   if (const char* e = std::getenv("QI_JIT_DEFINES")) {
     std::string d = e;
     size_t p = 0;
@@ -98,7 +88,7 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   o << "// generated evaluator: m=" << f.m << " T=" << f.T << " R=" << f.R << " G=" << f.G << "\n";
   o << "struct SpecEval {\n";
   // ---------------- containsQuorum ----------------
-  o << "  template <int POL, int QR = 0>\n  static __device__ __forceinline__ bool gfp(const LocalDev&, uint32_t (&X)[" << MW
+  o << "  template <int POL>\n  static __device__ __forceinline__ bool gfp(const LocalDev&, uint32_t (&X)[" << MW
     << "], uint32_t pol, uint32_t& rounds) {\n    (void)pol;\n";
   // |X| < qmin => empty fixpoint (LocalFlat::qmin), before any round
   o << "    { const uint32_t c = __popc(X[0])";
@@ -176,13 +166,6 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   o << "      bool same = true;\n";
   for (int w = 0; w < MW; ++w) o << "      n" << w << " &= X[" << w << "]; same &= (n" << w << " == X[" << w << "]);\n";
   o << "      if (same) return true;\n";
-  // survivors below qmin: the greatest fixpoint inside them is empty (LocalFlat::qmin)
-  o << "      if (QR || QI_QMIN_ROUND) { const uint32_t c = __popc(n0)";
-  for (int w = 1; w < MW; ++w) o << " + __popc(n" << w << ")";
-  o << "; const uint32_t q = POL == 0 ? " << f.qmin[0] << "u : (POL == 1 ? " << f.qmin[1] << "u : (pol ? " << f.qmin[1]
-    << "u : " << f.qmin[0] << "u));\n        if (c < q) {";
-  for (int w = 0; w < MW; ++w) o << " X[" << w << "] = 0u;";
-  o << " return false; } }\n";
   for (int w = 0; w < MW; ++w) o << "      X[" << w << "] = n" << w << ";\n";
   o << "    }\n  }\n";
   // ---------------- findBestNode ----------------
@@ -351,7 +334,7 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
 std::string cache_path(const std::string& src) {
   char key[32];
   const char* xf = std::getenv("QI_JIT_FLAGS");
-  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v3|" + (xf ? xf : "")));
+  std::snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(src + "|gfx950|-O3|v4|" + (xf ? xf : "")));
   return cache_dir() + "/" + key + ".co";
 }
 
@@ -391,7 +374,9 @@ std::vector<char> jit_compile(const std::string& src, std::string* log) {
   // the atomic optimizer rewrites every lane-0 atomic into a wave scan with an immediate
   // wait for its result; the kernel's lane-0 atomics are consumed an iteration later
   std::vector<std::string> optv = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pragma-once-outside-header",
-                                   "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"};
+                                   "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
+                                   // no packed FP32 VALU ops in device code (integer-only kernels)
+                                   "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"};
   if (const char* e = std::getenv("QI_JIT_FLAGS")) {  // diagnostics: extra compiler flags (space separated)
     std::istringstream is(e);
     std::string t;

@@ -100,10 +100,7 @@ __device__ __forceinline__ uint32_t extra_terms(const LocalDev& f, uint32_t t, c
 //     1 = available (visitor, cpp:354/368), 2 = per-lane `pol` (cooperative phase).
 // Same set as the reference's Gauss-Seidel sweep for monotone slices (every quorum set
 // has threshold >= 1); threshold-0 inputs are flagged nonmonotone by the host.
-// QR: test |survivors| >= qmin after every round too (the cooperative phase's jobs: with
-// |D| - 1 == qmin one round decides; measured 3 % slower on the main fixpoints, which keep
-// the entry test only unless QI_QMIN_ROUND).
-template <int MW, int TW, int POL, int QR = 0>
+template <int MW, int TW, int POL>
 __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32_t pol, uint32_t& rounds) {
   using R = TnRec<MW, TW>;
   {  // a non-empty fixpoint needs >= qmin vertices (LocalFlat::qmin): skip the rounds
@@ -165,22 +162,6 @@ __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32
       same &= (Xn[w] == X[w]);
     }
     if (same) return true;
-#if defined(QI_QMIN_ROUND) && QI_QMIN_ROUND
-    if (true) {
-#else
-    if (QR) {
-#endif
-      // survivors below qmin: the greatest fixpoint inside them is empty
-      uint32_t c = 0;
-#pragma unroll
-      for (int w = 0; w < MW; ++w) c += __popc(Xn[w]);
-      const uint32_t q = POL == 0 ? f.qmin0 : (POL == 1 ? f.qmin1 : (pol ? f.qmin1 : f.qmin0));
-      if (c < q) {
-#pragma unroll
-        for (int w = 0; w < MW; ++w) X[w] = 0u;
-        return false;
-      }
-    }
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = Xn[w];
   }
@@ -219,9 +200,9 @@ __device__ __forceinline__ uint32_t best_node(const LocalDev& f, const uint32_t 
 // specialised evaluator with the same interface is generated per FBAS (qi_jit.cpp).
 template <int MW, int TW>
 struct TableEval {
-  template <int POL, int QR = 0>
+  template <int POL>
   static __device__ __forceinline__ bool gfp(const LocalDev& f, uint32_t (&X)[MW], uint32_t pol, uint32_t& rounds) {
-    return dev::gfp<MW, TW, POL, QR>(f, X, pol, rounds);
+    return dev::gfp<MW, TW, POL>(f, X, pol, rounds);
   }
   static __device__ __forceinline__ uint32_t best(const LocalDev& f, const uint32_t (&Q)[MW], const uint32_t (&D)[MW],
                                                   uint32_t& zero_fallback) {
@@ -276,7 +257,6 @@ enum : int {
   C_OUT = 0,       // units written to units_out (spills + carried-over units)   [atomic]
   C_HEAD = 1,      // dynamic claims past the statically assigned range           [atomic]
   C_DONE = 2,      // used blocks that finished                                   [atomic]
-  C_XREC = 3,      // log records of stolen segments (after the n_in unit records) [atomic]
   C_EVX = 4,       // stack evictions granted from the shared output pool          [atomic]
   C_NIN = 32,      // input units of this launch (the previous block's C_OUT)
   C_LOGB = 33,     // first segment-log record of this launch
@@ -286,12 +266,7 @@ enum : int {
   C_HALT = 37,     // 1: this launch carried units over (its lanes ran out of budget with
                    // units left); the rest of the chain does nothing and the host sorts
                    // the frontier into preorder before it goes on
-  // donation queue of a persistent launch (SearchArgs::donate), own 128-B line:
-  C_DQLIVE = 64,   // u64: low 32 = slots reserved by donors (tail)                 [atomic]
-  C_DQHEAD = 96,   // slot tickets taken by waves (64 per claim), own line          [atomic]
-  C_DQFIN = 128,   // [16 shards, one 128-B line each]: units finished (no-return adds)
-  DQ_FIN_SHARDS = 16,
-  CTR_WORDS = 128 + 32 * 16,
+  CTR_WORDS = 64,
   HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6, HC_WORDS = 8
 };
 // Output capacity per launch: n_in (carried-over units) + per used lane SPILL_RESERVE(S)
@@ -303,6 +278,7 @@ enum : int {
 __host__ __device__ constexpr uint32_t spill_reserve(uint32_t smax) { return smax + 4u; }
 constexpr int TOT_SHARDS = 64;  // running totals: [TOT_SHARDS][16] u64, shard = block % 64
 
+constexpr int KEY_WORDS_MAX = 32;  // path-key words of the largest kernel shape (MW <= 32)
 struct SearchArgs {
   LocalDev f;
   const uint32_t* units_in;
@@ -320,37 +296,20 @@ struct SearchArgs {
   unsigned long long* best64;    // device-side best witness, best_pack(): exact when MW == 1,
                                  // the first 64 path bits (conservative pruning) otherwise
   uint32_t grow_budget;          // per-lane node budget while the frontier is below half the lanes
-  uint32_t ramp_budget;          // budget while the frontier is below 1/64 of the lanes (0: grow budget)
   uint32_t run_budget;
   uint32_t grace;                // extra steps per lane once the unit queue is dry
-  uint32_t steal_max;            // stacked entries a lane may take from busy lanes per launch
   uint32_t run_at;               // run budget once n_in >= run_at/8 of the resident lanes
-  uint32_t mid_budget;           // budget while run_at/8 <= n_in/lanes < full_at/8 (0: run budget)
-  uint32_t full_at;
   uint32_t evict_max;
   uint32_t half_m;
   uint32_t coop_slot;            // lanes per pending owner in the cooperative phase (pow2)
   uint32_t coop_slot_log2;
   uint32_t has_best;             // host-known best key (multiword) for pruning
   uint32_t best_depth;
-  uint32_t best_key[8];
-  uint32_t diag;                 // 0; opaque to the compiler (keeps QI_ABL_* repeats alive)
-  uint32_t coop_batch;           // parked quorum leaves that trigger a cooperative phase
-  uint32_t* gstack;              // QI_GSTACK builds: [blocks][64 lanes][SMAX][2MW+1] DFS stacks
-  // Persistent launches (donate = 1): a launch with the run budget has no node budget and
-  // no grace spill; once its input is claimed, idle lanes take subtrees that busy lanes
-  // donate through a queue in HBM (the bottom stack entry, like an eviction), and the
-  // launch ends when every unit of it has finished (search_body, "donation queue").
-  uint32_t donate;
-  uint32_t dq_cap;               // queue slots (one log record each, after the n_in records)
-  uint32_t dq_margin;            // ready units kept queued beyond the waiting claims
-  uint32_t dq_shift;             // a polling wave donates ceil(deficit / 2^dq_shift) entries
-  uint32_t epoch;                // this launch's publication tag (unique per launch)
-  uint32_t* dq_units;            // [dq_cap][unit words]
-  uint32_t* dq_flag;             // [dq_cap]: epoch of the launch that published the slot
+  uint32_t best_key[KEY_WORDS_MAX];
 };
+static_assert(sizeof(SearchArgs) <= 1024, "kernel argument block");
 
-enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u, FLAG_POOL = 8u, FLAG_DQ_CARRY = 32u, FLAG_DQ_TIMEOUT = 128u };
+enum : uint32_t { FLAG_OUT_OVERFLOW = 1u, FLAG_WIT_OVERFLOW = 2u, FLAG_POOL = 8u };
 
 // 64-bit preorder summary of a node (path key K, depth d) for the device-side best key:
 // MW == 1: (K0, d) -- exact order; MW > 1: (K0, K1) -- "strictly greater" still implies
@@ -364,6 +323,7 @@ __device__ __forceinline__ uint64_t best_pack(const uint32_t (&K)[MW], uint32_t 
 // preorder "strictly after" test of (K, d) vs (B, db): padded path bits, then depth.
 template <int MW>
 __device__ __forceinline__ bool after_key(const uint32_t (&K)[MW], uint32_t d, const uint32_t* B, uint32_t db) {
+  static_assert(MW <= 32, "path keys hold at most 32 words (SearchArgs::best_key, the engines' key buffers)");
 #pragma unroll
   for (int w = 0; w < MW; ++w) {
     if (K[w] != B[w]) return K[w] > B[w];
@@ -388,17 +348,11 @@ __device__ __forceinline__ void key_prefix_bit(uint32_t (&K)[MW], uint32_t de) {
 
 // Per-lane node budget of a launch from how well its input covers the resident lanes:
 // a small frontier grows (a few nodes per lane, then spill: more units next launch); a
-// frontier that covers most lanes runs long.  The middle tier (mid_budget, off when 0)
-// bounds launches that would otherwise run with part of the lanes idle.
+// frontier that covers most lanes runs long.
 __device__ __forceinline__ uint32_t launch_budget(const SearchArgs& a, uint32_t n_in) {
   const uint64_t lanes8 = (uint64_t)gridDim.x * WAVE;
   const uint64_t n8 = (uint64_t)n_in * 8u;
-  // a tiny frontier (the first launches from the root) digs deeper per lane, so each launch
-  // multiplies the frontier by more than the grow budget's ~3
-  if (a.ramp_budget && (uint64_t)n_in * 64u < lanes8 / 8u) return a.ramp_budget;
-  if (n8 < lanes8 * a.run_at) return a.grow_budget;
-  if (a.mid_budget && n8 < lanes8 * a.full_at) return a.mid_budget;
-  return a.run_budget;
+  return n8 < lanes8 * a.run_at ? a.grow_budget : a.run_budget;
 }
 
 // Wave-aggregated reservation of n (per lane, n < 2^NB) slots on a global counter: the
@@ -420,17 +374,11 @@ __device__ __forceinline__ uint32_t reserve(uint32_t n, uint32_t* counter, uint3
   return base + pre;
 }
 
-// LDS words of one search wavefront (search_body's carve-up below).  QI_GSTACK keeps the
-// DFS stack in global memory instead (L1/L2-resident, per-lane contiguous): the LDS then
-// no longer caps the resident waves per CU (7 at MW = 1), registers do.
-#ifndef QI_PK16
-#define QI_PK16 0  // 16-bit packed stack words: 9 waves/CU but measured 2-3 % slower (r02o)
-#endif
-template <int MW, int SMAX, bool GSTACK = false>
+// LDS words of one search wavefront (search_body's carve-up below).
+template <int MW, int SMAX>
 constexpr int search_lds_words() {
-  // DFS stack below the top entry: T', D' words + a packed (b, depth, |D|) word, which
-  // fits 16 bits when |SCC| <= 32 (halfword array: 640 B per level instead of 768)
-  return (GSTACK ? 0 : ((MW == 1 && QI_PK16) ? SMAX * (2 * WAVE + WAVE / 2) : SMAX * (2 * MW + 1) * WAVE))
+  // DFS stack below the top entry: T', D' words + a packed (b, depth, |D|) word per level
+  return SMAX * (2 * MW + 1) * WAVE
          + 2 * MW * WAVE                        // co_NE, co_VIS
          + (MW + 1) * WAVE                      // co_D, co_OWN
          + ((UnitLayout<MW>::DMAX + 3) / 4) * WAVE;  // D order
@@ -438,7 +386,7 @@ constexpr int search_lds_words() {
 
 // Diagnostic build only (QI_STAMPS, run-time specialised kernel with jit=3): per-wave
 // s_memtime sums of the loop sections, added into totals[8..15].  The production kernels
-// contain no stamps (MI355X guide §7 "In-kernel stamps": read shares, not lengths).
+// contain no stamps.
 #ifdef QI_STAMPS
 #define QI_STAMP(slot)                                                   \
   do {                                                                   \
@@ -457,15 +405,6 @@ constexpr int search_lds_words() {
   } while (0)
 #endif
 
-// QI_DONATE_CODE: the persistent-launch code, compiled only into specialised kernels built
-// for engines with donation on (its mere presence costs the relaunch kernel ~10 %: A/B r02d).
-// QI_QMIN_ROUND: a qmin test after every fixpoint round (measured 3 % slower: off).
-#ifndef QI_DONATE_CODE
-#define QI_DONATE_CODE 0
-#endif
-#ifndef QI_QMIN_ROUND
-#define QI_QMIN_ROUND 0
-#endif
 // single-round fixpoint when one root TN serves every vertex (generated evaluator)
 #ifndef QI_ONE_ROOT
 #define QI_ONE_ROOT 1
@@ -474,55 +413,15 @@ constexpr int search_lds_words() {
 #ifndef QI_FASTMIN
 #define QI_FASTMIN 1
 #endif
-// QI_COOP_LDS 1: the round-1 cooperative phase (owner slots and results through LDS)
-#ifndef QI_COOP_LDS
-#define QI_COOP_LDS 1  // the cross-lane form measured 3.82-3.85 vs 3.68 ms (r02c)
-#endif
+// packed D-order words per lane in LDS (a specialised kernel sizes them for its SCC)
 #ifndef QI_LDS_OW
 #define QI_LDS_OW 0
 #endif
-#ifndef QI_EARLY_CLAIM
-#define QI_EARLY_CLAIM 1
-#endif
-// per-round qmin test in the cooperative phase's fixpoints (QR above)
-#ifndef QI_COOP_QR
-#define QI_COOP_QR 0
-#endif
-// iterations between donation-queue polls of a persistent launch
-#ifndef QI_DQ_POLL_MASK
-#define QI_DQ_POLL_MASK 7
-#endif
-#ifndef QI_DQ_IDLE_MAX
-#define QI_DQ_IDLE_MAX (1u << 23)
-#endif
-#ifndef QI_INSTALL_AGE
-#define QI_INSTALL_AGE 0
-#endif
 // iterations between polls of the global queue head and the device-side best key
-// (round 2: 127; with the faster round-2 kernel, 32 -> 128 iterations measured 3.45-3.59
-// -> 3.20-3.24 ms per search and 1.50 -> 1.37 ms on planted_deep; 256/512/1024 slower,
-// profiles/r02/ab/poll_*)
+// (32 -> 128 iterations measured 3.45-3.59 -> 3.20-3.24 ms per search on the bench
+// workload and 1.50 -> 1.37 ms on planted_deep; 256/512/1024 slower)
 #ifndef QI_POLL_MASK
 #define QI_POLL_MASK 127
-#endif
-// The cooperative phase's LDS hand-offs stay inside one wavefront (blockDim == 64), whose
-// LDS operations complete in issue order: QI_COOP_WAVESYNC orders them with a wave-level
-// barrier instead of a workgroup barrier (whose fences also wait for outstanding global
-// memory operations).
-#ifndef QI_COOP_WAVESYNC
-#define QI_COOP_WAVESYNC 0
-#endif
-#if QI_COOP_WAVESYNC
-#define QI_COOP_SYNC()                                       \
-  do {                                                       \
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   \
-    __builtin_amdgcn_wave_barrier();                         \
-  } while (0)
-#else
-#define QI_COOP_SYNC() __syncthreads()
-#endif
-#ifndef QI_POLL_ASYNC
-#define QI_POLL_ASYNC 1
 #endif
 
 template <int MW, int TW, int SMAX, class EV>
@@ -544,21 +443,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   constexpr bool PREFETCH = UW <= 20;
   constexpr int FW = PREFETCH ? UW : 4;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-#ifdef QI_GSTACK
-  constexpr bool PK16 = false;
-  constexpr int SEW = SE;
-  uint32_t* const st = a.gstack + (size_t)blockIdx.x * (SMAX * SE * WAVE);  // [64][SMAX][SE]
-  uint16_t* const stpk = nullptr;
-  uint32_t* co_NE = lds;                                        // [MW][64] per pending rank
-#else
-  // |SCC| <= 32: the packed word is 16 bits (b < 32, depth < 64, |D| < 32) in its own
-  // halfword array, T' and D' are SEW = 2 words per level
-  constexpr bool PK16 = MW == 1 && QI_PK16;
-  constexpr int SEW = PK16 ? 2 * MW : SE;
-  uint32_t* st = lds;                                          // [SMAX][SEW][64]
-  uint16_t* const stpk = (uint16_t*)(st + SMAX * SEW * WAVE);   // [SMAX][64] (PK16)
-  uint32_t* co_NE = st + SMAX * SEW * WAVE + (PK16 ? SMAX * WAVE / 2 : 0);  // [MW][64] per pending rank
-#endif
+  uint32_t* st = lds;                                          // [SMAX][SE][64]
+  uint32_t* co_NE = st + SMAX * SE * WAVE;                      // [MW][64] per pending rank
   uint32_t* co_VIS = co_NE + MW * WAVE;                         // [MW][64] per pending rank
   uint32_t* co_D = co_VIS + MW * WAVE;                          // [MW][64] pending owners' D
   uint32_t* co_OWN = co_D + MW * WAVE;                          // [64] owner lane | dlen << 8
@@ -585,13 +471,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   const uint64_t spill_need = (uint64_t)n_in + (uint64_t)nb_used * WAVE * spill_reserve(SMAX);
   const uint32_t evict_pool = spill_need < (uint64_t)a.out_cap ? (uint32_t)((uint64_t)a.out_cap - spill_need) : 0u;
   const uint32_t budget = launch_budget(a, n_in);
-  // persistent launch: the first one with the run budget (the frontier covers the lanes)
-  const bool dmode = QI_DONATE_CODE && a.donate != 0u && budget == a.run_budget;
   {
     // the final spills, and at least evict_max evictions per used lane
     const uint64_t need_out = spill_need + (uint64_t)nb_used * WAVE * (uint64_t)a.evict_max;
-    const uint64_t need_log = (uint64_t)log_base + n_in +
-                              (dmode ? (uint64_t)a.dq_cap : (uint64_t)nb_used * WAVE * (a.steal_max + 1u));
+    const uint64_t need_log = (uint64_t)log_base + n_in;
     const bool stop = need_out > (uint64_t)a.out_cap || need_log > (uint64_t)a.log_cap;
     if (blockIdx.x == 0 && lane == 0) {
       cc[C_NIN] = n_in;
@@ -611,26 +494,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     if (stop || blockIdx.x >= nb_used) return;
   }
   uint32_t* const records = a.records + (size_t)log_base * RL::WORDS;
-#ifdef QI_GSTACK
-#define ST_IDX(lvl, w, ln) ((((ln) * SMAX) + (lvl)) * SE + (w))
-#else
-#define ST_IDX(lvl, w, ln) (((lvl) * SEW + (w)) * WAVE + (ln))
-#endif
+#define ST_IDX(lvl, w, ln) (((lvl) * SE + (w)) * WAVE + (ln))
 #define ST_(lvl, w) st[ST_IDX(lvl, w, lane)]
-  // packed (b, depth, |D| before b) of stack entry `pos` of lane `ln` (register format:
-  // b | depth << 8 | |D| << 17)
-  auto pk_get = [&](uint32_t pos, uint32_t ln) -> uint32_t {
-    if constexpr (PK16) {
-      const uint32_t h = stpk[pos * WAVE + ln];
-      return (h & 31u) | (((h >> 5) & 63u) << 8) | ((h >> 11) << 17);
-    } else {
-      return st[ST_IDX(pos, 2 * MW, ln)];
-    }
-  };
-  auto pk_set = [&](uint32_t pos, uint32_t v) {
-    if constexpr (PK16) stpk[pos * WAVE + lane] = (uint16_t)((v & 31u) | (((v >> 8) & 63u) << 5) | ((v >> 17) << 11));
-    else st[ST_IDX(pos, 2 * MW, lane)] = v;
-  };
 #define DOW_(w) dow[(w) * WAVE + lane]
   // byte i of this lane's D order (ds_write_b8 into the packed word)
   auto set_ord = [&](uint32_t i, uint32_t v) {
@@ -643,8 +508,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   for (int w = 0; w < MW; ++w) T[w] = D[w] = K[w] = 0;
   uint32_t depth = 0, dlen = 0;
   bool has = false, done = false;
-  bool park = false;  // the node is a quorum leaf waiting for the next cooperative phase
-  // top of the DFS stack in registers; `nst` entries below it in LDS (circular from sbase_)
+  // top of the DFS stack in registers (packed word: b | depth << 8 | |D| << 17); `nst`
+  // entries below it in LDS (circular from sbase_)
   uint32_t tT[MW], tD[MW], tpk = 0;
 #pragma unroll
   for (int w = 0; w < MW; ++w) tT[w] = tD[w] = 0;
@@ -654,53 +519,18 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     const uint32_t p = sbase_ + i;
     return p >= (uint32_t)SMAX ? p - (uint32_t)SMAX : p;
   };
-  uint32_t steps = 0, steals = 0;
+  uint32_t steps = 0;
   bool must_spill = false;  // an eviction found the pool empty: spill at the next iteration
-  uint32_t xpool_next = 0, xpool_end = 0;  // wave-uniform: claimed extra log record slots
-  uint32_t limit = dmode ? 0xFFFFFFFFu : budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
+  uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
   bool dry = false;         // wave-uniform: no unit left to claim (head >= n_in)
   uint32_t iter = 0;
-  // the next unit of this lane: claimed index + (PREFETCH) its words in registers
-  // A unit claimed at the end of iteration i is installed at the start of iteration
-  // i + 1 + QI_INSTALL_AGE (diagnostics; 0 measured best).
-  // fidx is the unit's log record index: its input index, or n_in + its queue slot (fdq)
-  bool fpend = false, fdq = false;
-  uint32_t fidx = 0, fage = 1;
+  // the next unit of this lane: claimed index (= its log record index) + (PREFETCH) its
+  // words in registers; installed at the start of the iteration after the lane ran out
+  bool fpend = false;
+  uint32_t fidx = 0;
   uint32_t fdat[FW];
 #pragma unroll
   for (int q = 0; q < FW; ++q) fdat[q] = 0;
-  // ---- donation queue state (persistent launches, dmode) ----
-  // donor: the bottom stack entry taken this iteration, written at the next iteration's
-  // start (slot = reserved tail base + rank), published (release, epoch tag) at its end
-  bool don_pend = false, flag_pend = false;
-  uint32_t dT[MW], dD[MW], dK[MW], dpk = 0, don_rank = 0, flag_slot = 0;
-#pragma unroll
-  for (int w = 0; w < MW; ++w) dT[w] = dD[w] = dK[w] = 0;
-  unsigned long long don_old = 0;  // lane 0: the tail reservation's returned value
-  bool don_issued = false;         // wave-uniform: a reservation is in flight
-  // claimant: a wave takes 64 slot tickets per atomic (like the input pool) and hands them
-  // to its idle lanes; a lane's slot tag is loaded when it gets the ticket and tested at
-  // each iteration's end until the donor has published it
-  bool dq_wait = false, dq_gone = false;
-  uint32_t dq_idx = 0, dq_seen = 0, dqh_old = 0;
-  uint32_t dqp_next = 0, dqp_end = 0;  // wave-uniform ticket pool
-  bool dq_req_any = false;             // wave-uniform: a ticket atomic is in flight
-
-  uint32_t fin_cnt = 0;            // units this lane finished since the last flush
-  uint32_t fin_v = 0, tail_v = 0, head_v = 0;  // poll loads (lanes 0-15: finished shards; lane 0)
-  uint32_t fin_sum = 0, poll_phase = 0;          // wave-uniform
-  bool live_zero = false, dq_full = false;  // wave-uniform, from the last queue poll
-  uint32_t dq_want = 0;                     // wave-uniform: entries to donate this iteration
-  uint32_t idle_iters = 0;                  // wave-uniform: consecutive iterations without work
-  uint32_t dg_idle = 0, dg_wait = 0, dg_evict = 0, dg_vol = 0, dg_atom = 0;  // diagnostics (wave-uniform)
-  unsigned long long* const live64 = (unsigned long long*)(cc + C_DQLIVE);
-  // Queue units cross CUs and XCDs inside the launch: every store and load of them is
-  // write-through / L1-bypassing (sc1, 16-B buffer ops), the donor wave drains its stores
-  // (vmcnt(0)) before the sc1 tag store, and the claimant loads only after its sc1 tag poll
-  // matched -- no L2 write-back or L1 invalidate (MI355X guide, inter-workgroup hand-offs).
-  const __amdgpu_buffer_rsrc_t dqr =
-      __builtin_amdgcn_make_buffer_rsrc(a.dq_units, 0, (int)min((uint64_t)a.dq_cap * UW * 4u, (uint64_t)0x7FFFFFF0u),
-                                        0x00020000);
   // current segment (one per installed unit)
   bool seg_open = false;
   uint32_t seg_idx = 0, seg_depth = 0, seg_count = 0, seg_evals = 0, seg_minq = 0, seg_zfb = 0;
@@ -716,59 +546,37 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   uint64_t best64 = ~0ull;
-  uint32_t poll_h = 0;     // QI_POLL_ASYNC: lane 0's pre-issued poll loads (the first poll,
-  uint64_t poll_b = ~0ull;  // at iteration 0, reads the ones issued here)
-#if QI_POLL_ASYNC
+  // lane 0's poll loads are issued one iteration before the poll that reads them, so
+  // their latency hides behind that iteration (the first poll, at iteration 0, reads these)
+  uint32_t poll_h = 0;
+  uint64_t poll_b = ~0ull;
   if (lane == 0) {
     poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     poll_b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-#endif
 
-  // words of the claimed unit: an input unit, or a queue slot (fdq)
-  auto unit_src = [&]() -> const uint32_t* {
-    return fdq ? a.dq_units + (size_t)(fidx - n_in) * UW : a.units_in + (size_t)fidx * UW;
-  };
-  auto load_unit = [&](uint32_t) {  // issue the loads for fidx/fdq (consumed at install)
+  auto load_unit = [&]() {  // issue the loads of unit fidx (consumed at install)
     if constexpr (PREFETCH) {
-      if (fdq) {
-        const uint32_t off = (fidx - n_in) * (uint32_t)(UW * 4);
+      const uint4* src = (const uint4*)(a.units_in + (size_t)fidx * UW);
 #pragma unroll
-        for (int q = 0; q < UW / 4; ++q) {
-          const qi_v4u v = __builtin_amdgcn_raw_buffer_load_b128(dqr, (int)(off + 16u * q), 0, 16);
-          fdat[4 * q + 0] = v.x;
-          fdat[4 * q + 1] = v.y;
-          fdat[4 * q + 2] = v.z;
-          fdat[4 * q + 3] = v.w;
-        }
-      } else {
-        const uint4* src = (const uint4*)unit_src();
-#pragma unroll
-        for (int q = 0; q < UW / 4; ++q) {
-          const uint4 v = src[q];
-          fdat[4 * q + 0] = v.x;
-          fdat[4 * q + 1] = v.y;
-          fdat[4 * q + 2] = v.z;
-          fdat[4 * q + 3] = v.w;
-        }
+      for (int q = 0; q < UW / 4; ++q) {
+        const uint4 v = src[q];
+        fdat[4 * q + 0] = v.x;
+        fdat[4 * q + 1] = v.y;
+        fdat[4 * q + 2] = v.z;
+        fdat[4 * q + 3] = v.w;
       }
     }
   };
   auto unit_word = [&](int wi) -> uint32_t {  // word wi of the claimed unit
-    if constexpr (PREFETCH) {
-      return fdat[wi];
-    } else {
-      if (fdq)
-        return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(dqr, (int)((fidx - n_in) * (uint32_t)(UW * 4) + 4u * wi), 0,
-                                                              16);
-      return unit_src()[wi];
-    }
+    if constexpr (PREFETCH) return fdat[wi];
+    else return a.units_in[(size_t)fidx * UW + wi];
   };
   // the statically assigned first unit of this lane (no atomic)
   if (blockIdx.x * WAVE + lane < n_in) {
     fidx = blockIdx.x * WAVE + lane;
     fpend = true;
-    load_unit(fidx);
+    load_unit();
   }
   uint32_t pool_next = 0, pool_end = 0;  // wave-uniform pool of claimed unit indices
   bool pool_dead = static_end >= n_in;
@@ -782,11 +590,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   for (int w = 0; w < RL::WORDS; ++w) rec[w] = 0;
   auto flush_record = [&]() {
     if (rec_pend) {
-#ifndef QI_ABL_NOREC  // diagnostics: no record stores (counts then only via running totals)
       uint32_t* r = records + (size_t)rec_idx * RL::WORDS;
 #pragma unroll
       for (int w = 0; w < RL::WORDS; ++w) r[w] = rec[w];
-#endif
       rec_pend = false;
     }
   };
@@ -801,7 +607,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     rec[MW + 4] = seg_zfb;
     rec_idx = seg_idx;
     rec_pend = true;
-    ++fin_cnt;  // the unit (input or queued) is finished for this launch
     tot_nodes += seg_count;
     tot_evals += seg_evals;
     tot_minq += seg_minq;
@@ -818,14 +623,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   };
 
   // write one unit (T, D given as masks, order = DOW[0..ol) + optional extra byte)
-  auto write_unit_to = [&](uint32_t* ubase, uint32_t ucap, uint32_t slot, const uint32_t (&UT)[MW],
-                           const uint32_t (&UD)[MW], const uint32_t (&UK)[MW], uint32_t udepth, uint32_t ol,
-                           int extra_b) {
-    if (slot >= ucap) {
+  auto write_unit = [&](uint32_t slot, const uint32_t (&UT)[MW], const uint32_t (&UD)[MW], const uint32_t (&UK)[MW],
+                        uint32_t udepth, uint32_t ol, int extra_b) {
+    if (slot >= a.out_cap) {
       atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
       return;
     }
-    uint32_t* u = ubase + (size_t)slot * UW;
+    uint32_t* u = a.units_out + (size_t)slot * UW;
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
       u[UL::T_ + w] = UT[w];
@@ -844,10 +648,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       u[UL::ORD + i] = word;
     }
   };
-  auto write_unit = [&](uint32_t slot, const uint32_t (&UT)[MW], const uint32_t (&UD)[MW], const uint32_t (&UK)[MW],
-                        uint32_t udepth, uint32_t ol, int extra_b) {
-    write_unit_to(a.units_out, a.out_cap, slot, UT, UD, UK, udepth, ol, extra_b);
-  };
   // a stack entry (T', D', packed) as a unit: the inclusion child it stands for
   auto write_entry = [&](uint32_t slot, const uint32_t (&ET)[MW], const uint32_t (&ED)[MW], uint32_t pk) {
     uint32_t UK[MW];
@@ -864,7 +664,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       ET[w] = ST_(pos, w);
       ED[w] = ST_(pos, MW + w);
     }
-    write_entry(slot, ET, ED, pk_get(pos, lane));
+    write_entry(slot, ET, ED, ST_(pos, 2 * MW));
   };
   // a claimed but not installed unit goes back out unchanged, its record zeroed
   auto write_claimed = [&](uint32_t slot) {
@@ -880,10 +680,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     for (int q = 0; q < UW; ++q) u[q] = unit_word(q);
   };
 
-  // claim the next units for the lanes that will need one in the next iteration (no node,
-  // no stacked entry left); the loads are in flight until the install.  Indices come
-  // from a wave-uniform pool of 64 claimed with one atomic (a returning atomic per
-  // iteration would cost a memory round trip every iteration).  Convergent.
   // D is a minimal quorum (cpp:283-285): credit cpp:184, |D| x cpp:192 and the visitor
   // (cpp:368); VIS = GFP(scc \ D) with outside vertices available.  A non-empty VIS is a
   // disjoint quorum: record the witness, the unit ends here (cpp:369-377).
@@ -911,12 +707,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     }
   };
 
+  // Claim the next units for the lanes whose current node is the last thing they hold (no
+  // top entry, empty stack): the unit's loads then have more than one iteration to land
+  // before the install's vmcnt wait.  Indices come from a wave-uniform pool of 64 claimed
+  // with one atomic (a returning atomic per iteration would cost a memory round trip every
+  // iteration).  Convergent.
   auto claim = [&]() {
-    // QI_EARLY_CLAIM: a lane whose current node is the last thing it holds claims its next
-    // unit already, so the unit's loads have more than one iteration to land (the install's
-    // vmcnt wait stalled on them: -110 cycles per wave-iteration in the pop/install
-    // section, 3.85 vs 3.96 ms per search, r02a)
-    bool want = !done && (QI_EARLY_CLAIM ? true : !has) && !fpend && !tvalid && nst == 0 && steps < limit;
+    bool want = !done && !fpend && !tvalid && nst == 0 && steps < limit;
     uint64_t wm = __ballot(want);
     while (wm) {
       if (pool_next >= pool_end) {
@@ -935,152 +732,20 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       const uint32_t r = rank_in(wm);
       if (want && r < avail) {
         fidx = pool_next + r;
-        fdq = false;
         fpend = true;
-        fage = 0;
         want = false;
-        load_unit(fidx);
+        load_unit();
       }
       pool_next += min((uint32_t)__popcll(wm), avail);
       wm = __ballot(want);
     }
-    if (dmode) {
-      // input claimed: idle lanes take queue tickets from the wave's pool; an empty pool
-      // asks for 64 more (one returning atomic, read at the next iteration's start)
-      if (pool_dead) {
-        const bool w2 = want && !dq_wait && !dq_gone && !live_zero;
-        const uint64_t m2 = __ballot(w2);
-        if (m2) {
-          const uint32_t avail = dqp_end - dqp_next, r = rank_in(m2);
-          if (w2 && r < avail) {
-            dq_idx = dqp_next + r;
-            if (dq_idx >= a.dq_cap) {
-              dq_gone = true;  // past the queue: never filled
-            } else {
-              dq_wait = true;
-              dq_seen = __hip_atomic_load(&a.dq_flag[dq_idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-          }
-          dqp_next += min((uint32_t)__popcll(m2), avail);
-          if ((uint32_t)__popcll(m2) > avail && !dq_req_any) {
-            if (lane == 0) dqh_old = atomicAdd(&cc[C_DQHEAD], (uint32_t)WAVE);
-            ++dg_atom;
-            dq_req_any = true;
-          }
-        }
-      }
-    } else if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
+    if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
       dry = true;
       limit = min(limit, steps + a.grace);
     }
   };
 
-  // Donation queue (dmode), once per iteration at its end: publish the units written at
-  // this iteration's start (release, then the epoch tag), and install-prefetch the queue
-  // slots whose tag has appeared (acquire).  The fence's wait covers stores issued a whole
-  // iteration earlier.  Convergent.
-  auto dq_service = [&]() {
-    const bool rdy = dq_wait && dq_seen == a.epoch;
-    if (__any(flag_pend)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 unit stores have landed
-      if (flag_pend) {
-        __hip_atomic_store(&a.dq_flag[flag_slot], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        flag_pend = false;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the unit loads below the tag poll
-    if (rdy) {
-      dq_wait = false;
-      fidx = n_in + dq_idx;
-      fdq = true;
-      fpend = true;
-      fage = 0;
-      load_unit(fidx);
-    } else if (dq_wait) {
-      dq_seen = __hip_atomic_load(&a.dq_flag[dq_idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-  // take this lane's bottom stack entry (the shallowest: the last of its range in
-  // preorder, like an eviction) for donation; its key and D-order prefix stay valid
-  // until the write at the next iteration's start
-  auto take_bottom = [&]() {
-    const uint32_t pos = spos(0);
-#pragma unroll
-    for (int w = 0; w < MW; ++w) {
-      dT[w] = ST_(pos, w);
-      dD[w] = ST_(pos, MW + w);
-      dK[w] = K[w];
-    }
-    dpk = pk_get(pos, lane);
-    key_prefix_bit<MW>(dK, (dpk >> 8) & 511u);
-    sbase_ = spos(1);
-    --nst;
-    don_pend = true;
-  };
-
   for (;;) {
-    // ---- (0) donation queue (dmode): claims and donations issued last iteration -------
-    if (dmode) {
-      if (dq_req_any) {  // 64 fresh tickets for this wave's idle lanes
-        dq_req_any = false;
-        dqp_next = lane0(dqh_old);
-        dqp_end = dqp_next + (uint32_t)WAVE;
-      }
-      if (don_issued) {  // reserved slots: write the donated units
-        don_issued = false;
-        const uint32_t base = lane0((uint32_t)don_old);
-        bool ovf = false;
-        if (don_pend) {
-          don_pend = false;
-          const uint32_t slot = base + don_rank;
-          if (slot < a.dq_cap) {
-            // the unit in 16-B write-through chunks: T, D, key, depth, |D|, then the D
-            // order (bytes past |D| are don't-care; the entry's own vertex merged in)
-            const uint32_t ol = dpk >> 17, ob = dpk & 255u, osh = 8u * (ol & 3u);
-            auto uw = [&](int i) -> uint32_t {
-              if (i < MW) return dT[i];
-              if (i < 2 * MW) return dD[i - MW];
-              if (i < 3 * MW) return dK[i - 2 * MW];
-              if (i == UL::DEPTH) return ((dpk >> 8) & 511u) + 1u;
-              if (i == UL::DLEN) return ol + 1u;
-              if (i >= UL::ORD && i < UL::ORD + OW) {
-                uint32_t word = DOW_(i - UL::ORD);
-                if ((uint32_t)(i - UL::ORD) == (ol >> 2)) word = (word & ~(0xFFu << osh)) | (ob << osh);
-                return word;
-              }
-              return 0u;
-            };
-            const uint32_t off = slot * (uint32_t)(UW * 4);
-#pragma unroll
-            for (int q = 0; q < UW / 4; ++q) {
-              const qi_v4u v = {uw(4 * q), uw(4 * q + 1), uw(4 * q + 2), uw(4 * q + 3)};
-              __builtin_amdgcn_raw_buffer_store_b128(v, dqr, (int)(off + 16u * q), 0, 16);
-            }
-            flag_pend = true;
-            flag_slot = slot;
-          } else {
-            ovf = true;
-            ++fin_cnt;  // the reserved slot is void; the entry leaves through units_out
-          }
-        }
-        const uint64_t om = __ballot(ovf);
-        if (om) {  // queue full: like an eviction (pool token, else this lane's spill reserve)
-          uint32_t tok = 0;
-          if (lane == 0) tok = atomicAdd(&cc[C_EVX], (uint32_t)__popcll(om));
-          tok = lane0(tok);
-          const bool granted = ovf && tok + rank_in(om) < evict_pool;
-          uint32_t total = 0;
-          const uint32_t slot = reserve<1>(ovf ? 1u : 0u, &cc[C_OUT], total);
-          if (ovf) {
-            write_unit(slot, dT, dD, dK, ((dpk >> 8) & 511u) + 1u, dpk >> 17, (int)(dpk & 255u));
-            if (!granted) {
-              must_spill = true;
-              atomicOr(&a.glob[1], FLAG_POOL);
-            }
-          }
-        }
-      }
-    }
     // ---- (1) lanes without a node: pop the top of stack, else install the next unit ----
     if (!done && !has) {
       if (tvalid) {
@@ -1111,7 +776,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
               tT[w] = ST_(pos, w);
               tD[w] = ST_(pos, MW + w);
             }
-            tpk = pk_get(pos, lane);
+            tpk = ST_(pos, 2 * MW);
           } else {
             tvalid = false;
           }
@@ -1119,7 +784,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
       if (!has) {
         if (seg_open) close_segment();  // the unit's subtree is done
-        if (fpend && fage >= QI_INSTALL_AGE && steps < limit) {  // install the claimed unit
+        if (fpend && steps < limit) {  // install the claimed unit
           uint32_t UK[MW];
 #pragma unroll
           for (int w = 0; w < MW; ++w) {
@@ -1154,181 +819,39 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
-    // ---- (1b) once this wave's pool is dry, idle lanes take the bottom (shallowest,
-    // largest) stacked entry of a busy lane of the wave.  That subtree is the last part of
-    // the donor's unit in preorder, so it becomes a segment of its own (log record after
-    // this launch's n_in unit records) and counts stay preorder-exact; the donor keeps
-    // the rest.  The k-th idle lane pairs with the k-th donor through an LDS slot.
-    if (pool_dead) {
-      const bool idle = !done && !has && !tvalid && nst == 0 && !fpend && steps < limit && steals < a.steal_max;
-      const uint64_t im = __ballot(idle);
-      if (im) {
-        const uint64_t gm = __ballot(nst > 0u);
-        const uint32_t np = min((uint32_t)__popcll(im), (uint32_t)__popcll(gm));
-        if (np) {
-          const uint32_t ri = rank_in(im), rg = rank_in(gm);
-          if (nst > 0u && rg < np) {  // donor: publish lane, entry position and key
-            co_OWN[rg] = lane | (spos(0) << 8);
-#pragma unroll
-            for (int w = 0; w < MW; ++w) co_D[w * WAVE + rg] = K[w];
-            sbase_ = spos(1);
-            --nst;
-          }
-          if (xpool_end - xpool_next < np) {  // extra record slots, 64 per atomic (the rest of
-            // an old pool is zero-filled: every slot of the log range must be written)
-            for (uint32_t i = xpool_next + lane; i < xpool_end; i += WAVE) {
-              uint32_t* r = records + (size_t)(n_in + i) * RL::WORDS;
-#pragma unroll
-              for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
-            }
-            uint32_t xb = 0;
-            if (lane == 0) xb = atomicAdd(&cc[C_XREC], (uint32_t)WAVE);
-            xpool_next = lane0(xb);
-            xpool_end = xpool_next + (uint32_t)WAVE;
-          }
-          const uint32_t xbase = xpool_next;
-          xpool_next += np;
-#ifdef QI_GSTACK
-          __threadfence_block();  // the donors' global stack stores, visible to the receivers
-#endif
-          if (idle && ri < np) {  // receiver: the entry becomes its unit
-            const uint32_t own = co_OWN[ri];
-            const uint32_t dl = own & 63u, pos = own >> 8;
-#pragma unroll
-            for (int w = 0; w < MW; ++w) {
-              T[w] = st[ST_IDX(pos, w, dl)];
-              D[w] = st[ST_IDX(pos, MW + w, dl)];
-              K[w] = co_D[w * WAVE + ri];
-            }
-            const uint32_t pk = pk_get(pos, dl);
-            const uint32_t b = pk & 255u, de = (pk >> 8) & 511u, dle = pk >> 17;
-            key_prefix_bit<MW>(K, de);
-            depth = de + 1;
-            dlen = dle + 1;
-            const uint32_t nw = (dle + 3) / 4;  // the donor's D order below the entry, then b
-            if constexpr (OW <= 8) {
-              uint32_t ow[OW];
-#pragma unroll
-              for (int i = 0; i < OW; ++i) ow[i] = ((uint32_t)i < nw) ? dow[i * WAVE + dl] : 0u;
-#pragma unroll
-              for (int i = 0; i < OW; ++i)
-                if ((uint32_t)i < nw) DOW_(i) = ow[i];
-            } else {
-              for (uint32_t i = 0; i < nw; ++i) DOW_(i) = dow[i * WAVE + dl];
-            }
-            set_ord(dle, b);
-            ++steals;
-            seg_idx = n_in + xbase + ri;
-            seg_open = true;
-            seg_count = seg_evals = seg_minq = seg_zfb = 0;
-#pragma unroll
-            for (int w = 0; w < MW; ++w) seg_K[w] = K[w];
-            seg_depth = depth;
-            nst = 0;
-            sbase_ = 0;
-            tvalid = false;
-            if (pruned(K, depth)) close_segment();
-            else has = true;
-          }
-        }
-      }
-    }
-
     QI_STAMP(0);  // pop / install
-    // lanes with nothing left: done (a claimed unit past the budget is spilled below)
-    if (dmode) {  // persistent: idle lanes stay until every unit of the launch has finished
-      if (!has && !tvalid && nst == 0 && !fpend && (live_zero || dq_gone)) done = true;
-    } else {  // a lane with nothing left is done once it cannot get a unit or steal any more
-      const bool wave_busy = __any(has || tvalid || nst > 0u);
-      if (!has && !tvalid && nst == 0 && !fpend &&
-          (steps >= limit || (pool_dead && (!wave_busy || steals >= a.steal_max))))
-        done = true;
-    }
+    // a lane with nothing left is done once it cannot get a unit any more (a claimed unit
+    // past the budget is spilled below)
+    if (!has && !tvalid && nst == 0 && !fpend && (steps >= limit || pool_dead)) done = true;
 
-    // Every 32 iterations poll the global head and the device-side best key (one
-    // blocking global load pair, kept off the per-iteration path).  Once no unit is left
-    // to claim anywhere, every lane gets a short grace period and then spills: the next
-    // launch spreads the remaining subtrees over all lanes instead of letting a few lanes
-    // grind through deep subtrees while the rest idle.
-    // Queue poll (dmode, every QI_DQ_POLL_MASK+1 iterations): flush this wave's finished
-    // count into the live word (returning: a consistent (tail, finished) pair) and read
-    // the claim head, one iteration before the values are used.  Live units = n_in +
-    // tail - finished; zero means nothing is held or queued anywhere, and nothing can be
-    // donated any more.  Waiting claims beyond the tail (+ margin) ask for donations.
-    if (dmode) {
-      // three phases, one per iteration: (A) flush this wave's finished count into its
-      // shard (no-return add) and load the 16 shards; (B) sum them, then load the tail and
-      // the ticket head; (C) evaluate.  The finished counts are read before the tail, and
-      // both only grow, so live = n_in + tail - finished is never below the true count at
-      // the time of the shard loads: zero means nothing is held or queued anywhere, and
-      // nothing can be donated any more.  Tickets beyond the tail ask for donations.
-      if (poll_phase == 2u) {
-        poll_phase = 0;
-        const uint32_t tail = lane0(tail_v), hd = lane0(head_v);
-        live_zero = (uint64_t)n_in + tail == (uint64_t)fin_sum;
-        dq_full = tail >= a.dq_cap;
-        const int32_t deficit = (int32_t)(hd - tail) + (int32_t)a.dq_margin;
-        dq_want = (deficit > 0 && (dry || pool_dead) && !dq_full) ? (uint32_t)WAVE : 0u;
-      } else if (poll_phase == 1u) {
-        poll_phase = 2;
-        uint32_t fsum = 0;
-#pragma unroll
-        for (int l = 0; l < DQ_FIN_SHARDS; ++l) fsum += (uint32_t)__builtin_amdgcn_readlane((int)fin_v, l);
-        fin_sum = fsum;
-        if (lane == 0) {
-          tail_v = __hip_atomic_load((uint32_t*)live64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          head_v = __hip_atomic_load(&cc[C_DQHEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else {
-        const bool waiting = __any(dq_wait || (!has && !tvalid && !fpend && !done));
-        if (((iter + 1u) & (waiting ? (uint32_t)QI_DQ_POLL_MASK : 31u)) == 0u) {
-          poll_phase = 1;
-          uint32_t fs = 0;
-#pragma unroll
-          for (int b = 0; b < 8; ++b) fs += (uint32_t)__popcll(__ballot((fin_cnt >> b) & 1u)) << b;
-          fin_cnt = 0;
-          if (lane == 0 && fs) atomicAdd(&cc[C_DQFIN + 32 * (blockIdx.x & (DQ_FIN_SHARDS - 1))], fs);
-          if (lane < (uint32_t)DQ_FIN_SHARDS)
-            fin_v = __hip_atomic_load(&cc[C_DQFIN + 32 * lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ++dg_atom;
-        }
-      }
-    }
-#if QI_POLL_ASYNC
-    // the loads are issued one iteration before the poll that reads them, so their latency
-    // hides behind that iteration (the values are at most one iteration older)
+    // Every QI_POLL_MASK + 1 iterations poll the global head and the device-side best key
+    // (loads issued one iteration ahead).  Once no unit is left to claim anywhere, every
+    // lane gets a short grace period and then spills: the next launch spreads the
+    // remaining subtrees over all lanes instead of letting a few lanes grind through deep
+    // subtrees while the rest idle.
     if (((iter + 1u) & (uint32_t)QI_POLL_MASK) == 0u && lane == 0) {
       poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       poll_b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#endif
     if ((iter++ & (uint32_t)QI_POLL_MASK) == 0u) {
       uint32_t h = 0;
       uint64_t b = ~0ull;
-#if QI_POLL_ASYNC
       if (lane == 0) {
         h = static_end + poll_h;
         b = poll_b;
       }
-#else
-      if (lane == 0) {
-        h = static_end + __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#endif
       h = lane0(h);
       best64 = lane0(b);
       if (!dry && h >= n_in) {
         dry = true;
-        if (!dmode) limit = min(limit, steps + a.grace);
+        limit = min(limit, steps + a.grace);
       }
     }
 
-    QI_STAMP(1);  // claims + polls
+    QI_STAMP(1);  // polls
     // ---- (3) budget exhausted: spill current node, top, stack and claimed unit ---------
     {
-      const bool spill = (has && !park && (steps >= limit || must_spill)) ||
-                         (!has && fpend && steps >= limit);
+      const bool spill = (has && (steps >= limit || must_spill)) || (!has && fpend && steps >= limit);
       if (__any(spill)) {
         uint32_t total = 0;
         const uint32_t n = spill ? (has ? 1u : 0u) + (tvalid ? 1u : 0u) + nst + (fpend ? 1u : 0u) : 0u;
@@ -1337,10 +860,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           if (has) write_unit(slot++, T, D, K, depth, dlen, -1);
           if (tvalid) write_entry(slot++, tT, tD, tpk);
           for (uint32_t i = nst; i > 0; --i) write_lds_entry(slot++, spos(i - 1));
-          if (fpend) {
-            write_claimed(slot++);
-            ++fin_cnt;  // a claimed unit leaves this launch unprocessed
-          }
+          if (fpend) write_claimed(slot++);
           nst = 0;
           tvalid = false;
           fpend = false;
@@ -1350,14 +870,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
     }
-    // (a done lane may still hold a written, unpublished queue unit: publish it first)
-    if (!__any(!done || flag_pend)) break;
+    if (!__any(!done)) break;
 
     QI_STAMP(2);  // spill
     // ---- (4) one search node per active lane (cpp:258-345) ---------------------------
     ++wave_iters;
     bool pending = false;
-    bool active = has && !park;
+    bool active = has;
     if (active) {
       ++steps;
       ++seg_count;
@@ -1381,18 +900,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = active2 ? (T[w] | D[w]) : 0u;
     const bool qne = EV::template gfp<0>(f, X, 0u, rounds);  // cpp:301
-#ifdef QI_ABL_GFP
-    {  // ablation: repeat both fixpoints on the same inputs (marginal cost measurement)
-      uint32_t Z[MW];
-#pragma unroll
-      for (int w = 0; w < MW; ++w) Z[w] = (active ? D[w] : 0u) ^ a.diag;
-      const bool r1 = EV::template gfp<0>(f, Z, 0u, rounds);
-#pragma unroll
-      for (int w = 0; w < MW; ++w) Z[w] = (active2 ? (T[w] | D[w]) : 0u) ^ a.diag;
-      const bool r2 = EV::template gfp<0>(f, Z, 0u, rounds);
-      if ((r1 ^ r2) && a.diag == 0x5EEDu) atomicOr(&a.glob[1], 64u);
-    }
-#endif
     QI_STAMP(3);  // the two fixpoints
     bool push = false;
     uint32_t pb = 0;
@@ -1408,14 +915,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         has = false;
       } else {
         pb = EV::best(f, X, D, seg_zfb);  // cpp:317
-#ifdef QI_ABL_BEST
-        {
-          uint32_t Z[MW], zz = 0;
-#pragma unroll
-          for (int w = 0; w < MW; ++w) Z[w] = X[w] ^ a.diag;
-          if (EV::best(f, Z, D, zz) != pb && a.diag == 0x5EEDu) atomicOr(&a.glob[1], 64u);
-        }
-#endif
 #pragma unroll
         for (int w = 0; w < MW; ++w) X[w] &= ~D[w];
         X[pb >> 5] &= ~(1u << (pb & 31u));  // toRemove' = Q \ D \ {b} (cpp:330-334)
@@ -1428,17 +927,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // exclusion branch (cpp:336): same D, T = T', key bit 0.
     {
       const bool evict = push && tvalid && nst == (uint32_t)SMAX;
-      bool forced = false;  // no pool slot: the old top leaves through this lane's spill reserve
-      if (dmode && !dq_full) {  // persistent: the evicted entry is donated to the queue
-        if (evict) take_bottom();
-        dg_evict += (uint32_t)__popcll(__ballot(evict));
-      } else if (__any(evict)) {
+      if (__any(evict)) {
         const uint64_t em = __ballot(evict);
         uint32_t tok = 0;
         if (lane == 0) tok = atomicAdd(&cc[C_EVX], (uint32_t)__popcll(em));
         tok = lane0(tok);
         const bool granted = evict && tok + rank_in(em) < evict_pool;
-        forced = evict && !granted;
+        const bool forced = evict && !granted;  // no pool slot: the old top leaves through this lane's spill reserve
         uint32_t total = 0;
         const uint32_t slot = reserve<1>(evict ? 1u : 0u, &cc[C_OUT], total);
         if (granted) {
@@ -1460,7 +955,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             ST_(pos, w) = tT[w];
             ST_(pos, MW + w) = tD[w];
           }
-          pk_set(pos, tpk);
+          ST_(pos, 2 * MW) = tpk;
           ++nst;
         }
 #pragma unroll
@@ -1476,54 +971,12 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
-    if (dmode) {
-      // voluntary donations: a poll saw waiting claims (or a short queue); lanes with an
-      // entry below their top give their bottom entry, dq_want per wave
-      if (dq_want) {  // (a lane whose only entry is its top gives that, keeping its node)
-        const bool cand = (nst > 0u || (tvalid && has)) && !don_pend;
-        const uint64_t cm = __ballot(cand);
-        dg_vol += min((uint32_t)__popcll(cm), dq_want);
-        if (cand && rank_in(cm) < dq_want) {
-          if (nst > 0u) {
-            take_bottom();
-          } else {
-#pragma unroll
-            for (int w = 0; w < MW; ++w) {
-              dT[w] = tT[w];
-              dD[w] = tD[w];
-              dK[w] = K[w];
-            }
-            dpk = tpk;
-            key_prefix_bit<MW>(dK, (dpk >> 8) & 511u);
-            tvalid = false;
-            don_pend = true;
-          }
-        }
-        dq_want = 0;
-      }
-      // one tail reservation per wave for this iteration's donations and evictions
-      const uint64_t dm = __ballot(don_pend);
-      if (dm) {
-        don_rank = rank_in(dm);
-        if (lane == 0) don_old = atomicAdd(live64, (unsigned long long)__popcll(dm));
-        ++dg_atom;
-        don_issued = true;
-      }
-    }
-    // the unit loads of lanes that became free: in flight during the cooperative phase
+    // the unit loads of lanes that became free: in flight during the quorum-leaf phase
     // below (the install waits on vmcnt, which counts stores and loads in issue order)
-    if (dmode) dq_service();
     flush_record();
     claim();
     QI_STAMP(4);  // findBestNode + push
-    // ---- (5) quorum leaves: isMinimalQuorum + visitor, wave-cooperative --------------
-    // Every pending lane (GFP(D) != ∅, cpp:281) needs |D| single-removal fixpoints
-    // (isMinimalQuorum, cpp:188-198) and the complement check of the visitor (cpp:368).
-    // Done per lane they would serialise the wave (the first removable vertex sits at a
-    // ~uniform position of the D order), so they are spread over the wave in fixed slots
-    // of S = a.coop_slot lanes per pending lane: lane l serves owner (l / S) of the
-    // current pass, job k = l % S (+ chunk offset when |D|+1 > S).  The owner's D, lane
-    // and |D| arrive through an LDS slot, results by one LDS ds_or per successful job.
+    // ---- (5) quorum leaves: isMinimalQuorum + visitor ---------------------------------
     // Quorum leaves with |D| - 1 < qmin: no D \ {v} can hold a quorum (LocalFlat::qmin),
     // so D is minimal without evaluating them (still credited, as the reference makes the
     // calls); only the visitor's fixpoint remains, evaluated here per lane.
@@ -1605,19 +1058,22 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 #endif
-    // Quorum leaves park until coop_batch of them are waiting (one phase then serves up
-    // to 64 / S owners per pass) or no lane of the wave has a node left to search.
-    park = park || pending;
-    const uint64_t pk_m = __ballot(park);
-    const uint64_t pm = (pk_m && ((uint32_t)__popcll(pk_m) >= a.coop_batch || !__any(has && !park))) ? pk_m : 0ull;
-#if QI_COOP_LDS
+    // Remaining quorum leaves (|D| >= qmin + 2), wave-cooperative: every pending lane needs
+    // |D| single-removal fixpoints (isMinimalQuorum, cpp:188-198) and the complement check
+    // of the visitor (cpp:368).  Done per lane they would serialise the wave (the first
+    // removable vertex sits at a ~uniform position of the D order), so they are spread over
+    // the wave in fixed slots of S = a.coop_slot lanes per pending lane: lane l serves owner
+    // (l / S) of the current pass, job k = l % S (+ chunk offset when |D|+1 > S).  The
+    // owner's D, lane and |D| arrive through an LDS slot, results by one LDS ds_or per
+    // successful job.
+    const uint64_t pm = __ballot(pending);
     if (pm) {
       ++coop_phases;
       const uint32_t npend = (uint32_t)__popcll(pm);
       const uint32_t r = rank_in(pm);
       const uint32_t S = a.coop_slot, lgS = a.coop_slot_log2;
       const uint32_t P = (uint32_t)WAVE >> lgS;  // owners per pass
-      if (park) {  // owner slot r: results zeroed, D / lane / |D| published
+      if (pending) {  // owner slot r: results zeroed, D / lane / |D| published
 #pragma unroll
         for (int w = 0; w < MW; ++w) {
           co_NE[w * WAVE + r] = 0u;
@@ -1626,7 +1082,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
         co_OWN[r] = lane | (dlen << 8);
       }
-      QI_COOP_SYNC();
+      __syncthreads();
       for (uint32_t q0 = 0; q0 < npend; q0 += P) {
         const uint32_t oi = q0 + (lane >> lgS);
         const uint32_t oc = min(oi, (uint32_t)WAVE - 1u);  // slots >= npend: stale, masked by `act`
@@ -1651,15 +1107,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             else Y[w] = Dr[w];
           }
           if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
-#ifdef QI_ABL_COOP
-          {
-            uint32_t Z[MW];
-#pragma unroll
-            for (int w = 0; w < MW; ++w) Z[w] = Y[w] ^ a.diag;
-            if (EV::template gfp<2>(f, Z, vis ? 1u : 0u, rounds) && a.diag == 0x5EEDu) atomicOr(&a.glob[1], 64u);
-          }
-#endif
-          const bool ne = EV::template gfp<2, QI_COOP_QR>(f, Y, vis ? 1u : 0u, rounds);
+          const bool ne = EV::template gfp<2>(f, Y, vis ? 1u : 0u, rounds);
           if (act && !vis && ne) atomicOr(&co_NE[(k >> 5) * WAVE + oi], 1u << (k & 31u));
           if (vis) {
 #pragma unroll
@@ -1668,9 +1116,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           if (c0 + S > a.half_m) break;
         }
       }
-      QI_COOP_SYNC();
-      if (park) {
-        park = false;
+      __syncthreads();
+      if (pending) {
         uint32_t ne_any = 0, vis_any = 0;
         uint32_t NE[MW], VIS[MW];
 #pragma unroll
@@ -1691,150 +1138,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           seg_evals += 2u + pos;  // cpp:184 + (pos+1) x cpp:192
         }
       }
-      QI_COOP_SYNC();
-    }
-#else
-    // Cross-lane form of the same phase: the owners of a pass are the next P pending lanes in
-    // lane order (their rank order); every lane reads its group owner's D and |D| with
-    // readlanes (SGPR values, no LDS round trip), only the removed vertex comes from the
-    // owner's D-order bytes in LDS; each chunk's results are one ballot, from which every
-    // owner shifts out its own S bits, and the visitor's survivors reach the owner with one
-    // lane permute.
-    if (pm) {
-      ++coop_phases;
-      const uint32_t npend = (uint32_t)__popcll(pm);
-      const uint32_t r = rank_in(pm);
-      const uint32_t S = a.coop_slot, lgS = a.coop_slot_log2;
-      const uint32_t P = (uint32_t)WAVE >> lgS;  // owners per pass
-      const uint32_t grp = lane >> lgS;          // this lane's slot group
-      const uint64_t maskS = S >= 64u ? ~0ull : ((1ull << S) - 1ull);
-      uint32_t NE[MW], VIS[MW];
-#pragma unroll
-      for (int w = 0; w < MW; ++w) NE[w] = VIS[w] = 0u;
-      uint64_t rem = pm;  // wave-uniform: pending lanes not yet served
-      for (uint32_t q0 = 0; q0 < npend; q0 += P) {
-        uint32_t ol = 0, dl = 0;
-        bool gv = false;  // this lane's group has an owner in this pass
-        uint32_t Dr[MW];
-#pragma unroll
-        for (int w = 0; w < MW; ++w) Dr[w] = 0u;
-        for (uint32_t gi = 0; gi < P && rem; ++gi) {
-          const uint32_t o = (uint32_t)__builtin_ctzll(rem);
-          rem &= rem - 1ull;
-          const uint32_t odl = (uint32_t)__builtin_amdgcn_readlane((int)dlen, (int)o);
-          const bool mine = grp == gi;
-          ol = mine ? o : ol;
-          dl = mine ? odl : dl;
-          gv = gv || mine;
-#pragma unroll
-          for (int w = 0; w < MW; ++w) {
-            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)D[w], (int)o);
-            Dr[w] = mine ? x : Dr[w];
-          }
-        }
-        const bool own = park && r >= q0 && r < q0 + P;  // an owner served in this pass
-        const uint32_t og = r - q0;                       // its group (when own)
-        for (uint32_t c0 = 0; c0 <= a.half_m; c0 += S) {  // jobs 0..|D| (|D| <= half_m)
-          const uint32_t k = c0 + (lane & (S - 1u));
-          const bool act = gv && k <= dl;
-          const bool vis = act && k == dl;
-          // job k < |D| removes the k-th vertex of the owner's D order (its LDS bytes);
-          // NE is indexed by that position, so isMinimal's first hit is one ctz
-          uint32_t v = 0;
-          if (act && !vis) v = (dow[(k >> 2) * WAVE + ol] >> (8u * (k & 3u))) & 255u;
-          uint32_t Y[MW];
-#pragma unroll
-          for (int w = 0; w < MW; ++w) {
-            if (!act) Y[w] = 0u;
-            else if (vis) Y[w] = EV::scc_word(f, w) & ~Dr[w];  // visitor: scc \ Q, outside available
-            else Y[w] = Dr[w];
-          }
-          if (act && !vis) Y[v >> 5] &= ~(1u << (v & 31u));  // isMinimal: D \ {v}
-          const bool ne = EV::template gfp<2, QI_COOP_QR>(f, Y, vis ? 1u : 0u, rounds);
-          const uint64_t M = __ballot(act && !vis && ne);
-          if (own) {  // this owner's jobs c0 .. c0+S-1 are bits [og*S, og*S+S) of M
-            const uint64_t cb = (M >> (og << lgS)) & maskS;
-            if (S <= 32u) {
-              const uint32_t wi = c0 >> 5, bits = (uint32_t)cb << (c0 & 31u);
-#pragma unroll
-              for (int w = 0; w < MW; ++w)
-                if ((uint32_t)w == wi) NE[w] |= bits;
-            } else {
-#pragma unroll
-              for (int w = 0; w < MW; ++w) {
-                if ((uint32_t)w == (c0 >> 5)) NE[w] |= (uint32_t)cb;
-                if ((uint32_t)w == (c0 >> 5) + 1u) NE[w] |= (uint32_t)(cb >> 32);
-              }
-            }
-          }
-          // the visitor's survivors sit in lane og*S + (|D| - c0) of the chunk holding job |D|
-          const bool vin = own && dlen >= c0 && dlen < c0 + S;
-          const int src = vin ? (int)((og << lgS) + (dlen - c0)) : (int)lane;
-#pragma unroll
-          for (int w = 0; w < MW; ++w) {
-            const uint32_t y = (uint32_t)__shfl((int)Y[w], src);
-            if (vin) VIS[w] = y;
-          }
-          if (c0 + S > a.half_m) break;
-        }
-      }
-      if (park) {
-        park = false;
-        uint32_t ne_any = 0, vis_any = 0;
-#pragma unroll
-        for (int w = 0; w < MW; ++w) {
-          ne_any |= NE[w];
-          vis_any |= VIS[w];
-        }
-        has = false;
-        if (!ne_any) {  // minimal quorum (cpp:283-285)
-          minimal_quorum(VIS, vis_any != 0u);
-        } else {  // not minimal: isMinimal stops at the first removable vertex in D order
-          uint32_t pos = 0;
-#pragma unroll
-          for (int w = MW - 1; w >= 0; --w)
-            if (NE[w]) pos = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(NE[w]);
-          seg_evals += 2u + pos;  // cpp:184 + (pos+1) x cpp:192
-        }
-      }
-    }
-#endif
-    QI_STAMP(5);  // quorum-leaf phase
-    if (pm) {  // lanes freed by the cooperative phase
-      flush_record();
+      __syncthreads();
+      flush_record();  // lanes freed by the cooperative phase
       claim();
     }
-    // a persistent wave with no work left waits for donations: yield the issue slots
-    if (dmode) {
-      dg_wait += (uint32_t)__popcll(__ballot(dq_wait));
-      if (!__any(has || tvalid || fpend)) {
-        ++dg_idle;
-        __builtin_amdgcn_s_sleep(2);
-        // safety net: a wave idle this long means the queue protocol is broken (never in
-        // a correct run: lanes holding work donate on demand); fail loudly, do not hang
-        if (++idle_iters > (uint32_t)QI_DQ_IDLE_MAX) {
-          if (lane == 0) atomicOr(&a.glob[1], FLAG_DQ_TIMEOUT);
-          done = true;
-        }
-      } else {
-        idle_iters = 0;
-      }
-    }
-    ++fage;
+    QI_STAMP(5);  // quorum-leaf phase
   }
   flush_record();
-  if (dmode) {  // finished units not yet counted, and input units this wave claimed but never took
-    uint32_t fs = 0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) fs += (uint32_t)__popcll(__ballot((fin_cnt >> b) & 1u)) << b;
-    if (pool_next < pool_end) fs += pool_end - pool_next;
-    if (lane == 0 && fs) atomicAdd(&cc[C_DQFIN + 32 * (blockIdx.x & (DQ_FIN_SHARDS - 1))], fs);
-  }
-  for (uint32_t i = xpool_next + lane; i < xpool_end; i += WAVE) {  // unused extra record slots
-    uint32_t* r = records + (size_t)(n_in + i) * RL::WORDS;
-#pragma unroll
-    for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
-  }
 
   // indices of this wave's pool that no lane took: carry the units over unchanged
   if (pool_next < pool_end) {
@@ -1878,16 +1188,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     atomicAdd(&tt[5], (unsigned long long)tot_fetched);
     atomicAdd(&tt[6], (unsigned long long)wave_iters);
     atomicAdd(&tt[7], (unsigned long long)coop_phases);
-#if !defined(QI_STAMPS) && QI_DONATE_CODE
-    if (dmode) {  // persistent-launch counters (stamps words; no stamps in this build)
-      atomicAdd(&tt[8], (unsigned long long)dg_idle);     // wave-iterations without work
-      atomicAdd(&tt[9], (unsigned long long)dg_wait);     // lane-iterations waiting on a queue slot
-      atomicAdd(&tt[10], (unsigned long long)dg_evict);   // evictions donated
-      atomicAdd(&tt[11], (unsigned long long)dg_vol);     // voluntary donations
-      atomicAdd(&tt[12], (unsigned long long)dg_atom);    // queue atomics issued by this wave
-      atomicAdd(&tt[13], (unsigned long long)wave_iters); // wave-iterations in persistent launches
-    }
-#endif
 #ifdef QI_STAMPS
     for (int q = 0; q < 6; ++q) atomicAdd(&tt[8 + q], (unsigned long long)stamp_sum[q]);
     atomicAdd(&tt[14], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - wave_t0));  // 100 MHz ticks
@@ -1926,47 +1226,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
         }
       }
-      uint32_t xr = 0;
-      if (dmode) {
-        // queue slots: their records follow the n_in unit records; slots nobody claimed
-        // (every lane spilled or gave up first) carry over like never-claimed input
-        uint64_t lv = 0;
-        uint32_t dh = 0;
-        if (lane == 0) {
-          lv = atomicAdd(live64, 0ull);
-          dh = atomicAdd(&cc[C_DQHEAD], 0u);
-        }
-        lv = lane0((uint64_t)lv);
-        dh = lane0(dh);
-        xr = min((uint32_t)lv, a.dq_cap);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other waves' queue units
-        const uint32_t dleft = dh < xr ? xr - dh : 0u;
-        for (uint32_t i = lane; i < dleft; i += WAVE) {
-          uint32_t* r = records + (size_t)(n_in + dh + i) * RL::WORDS;
-          for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
-          const uint32_t dst = out + left + i;
-          if (dst < a.out_cap) {
-            const uint4* s4 = (const uint4*)(a.dq_units + (size_t)(dh + i) * UW);
-            uint4* d4 = (uint4*)(a.units_out + (size_t)dst * UW);
-            for (int q = 0; q < UW / 4; ++q) d4[q] = s4[q];
-          } else {
-            atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
-          }
-        }
-        if (dleft && lane == 0) atomicOr(&a.glob[1], FLAG_DQ_CARRY);
-        out += dleft;
-      } else {
-        if (lane == 0) xr = atomicAdd(&cc[C_XREC], 0u);
-        xr = lane0(xr);
-      }
       if (lane == 0) {
         // never-claimed units: the global queue outlived every lane's node budget
         cc[C_HALT] = left ? 1u : 0u;
         a.host_ctr[HC_HALT] = left ? 1u : 0u;
         out += left;
         if (out != lane0_out) atomicExch(&cc[C_OUT], out);
-        cc[C_LOGN] = log_base + n_in + xr;
-        a.host_ctr[HC_LOGN] = log_base + n_in + xr;
+        cc[C_LOGN] = log_base + n_in;
+        a.host_ctr[HC_LOGN] = log_base + n_in;
         a.host_ctr[HC_OUT] = out;
         a.host_ctr[HC_NIN] = n_in;
         a.host_ctr[HC_LOGB] = log_base;

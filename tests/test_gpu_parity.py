@@ -514,65 +514,6 @@ def test_grow_deal_strided_random_witness(seed):
                                                                  r["evals"] - r["scc_evals"], r["minq"])
 
 
-# ---- intra-wave stealing (off by default; QI_STEAL = entries per lane per launch) ---------
-@pytest.mark.parametrize("name", ["tiered_5", "tiered_6", "broken", "planted_5_96", "tiered_5_shuffled"])
-def test_stealing_exact(name, monkeypatch):
-    monkeypatch.setenv("QI_STEAL", "16")
-    text = _text_for(name)
-    r = GOLD[name] if name in GOLD else Oracle().load(text).solve()
-    for jit in (1, 2):
-        d = qa.FBAS(text).solve_stats(jit=jit, grow_budget=2, run_budget=64)
-        assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"], r["evals"], r["minq"])
-        if not r["verdict"]:
-            assert d["q1"] == r["q1"] and d["q2"] == r["q2"]
-
-
-# ---- parked quorum leaves (QI_COOP_BATCH = leaves per cooperative phase; default 1) -------
-@pytest.mark.parametrize("batch", ["2", "4"])
-@pytest.mark.parametrize("name", ["tiered_6", "broken", "planted_5_96", "tiered_5_shuffled"])
-def test_coop_batch_exact(name, batch, monkeypatch):
-    monkeypatch.setenv("QI_COOP_BATCH", batch)
-    text = _text_for(name)
-    r = GOLD[name] if name in GOLD else Oracle().load(text).solve()
-    for jit in (1, 2):
-        d = qa.FBAS(text).solve_stats(jit=jit, grow_budget=2, run_budget=64)
-        assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (r["verdict"], r["nodes"], r["evals"], r["minq"])
-        if not r["verdict"]:
-            assert d["q1"] == r["q1"] and d["q2"] == r["q2"]
-
-
-# ---- persistent launches (QI_DONATE=1; off by default) --------------------------------------
-# The first launch with the run budget runs until all of its units are finished: idle lanes
-# take subtrees busy lanes donate through a queue in HBM (sc1 hand-offs).  QI_RUN_AT=0 makes
-# the root launch persistent, so even small trees spread through the queue; QI_DQ_CAP=64
-# overflows the queue (void reservations, evictions and donations through units_out, carry).
-@pytest.mark.parametrize("env", [{}, {"QI_RUN_AT": "0"}, {"QI_RUN_AT": "0", "QI_DQ_CAP": "64"},
-                                 {"QI_RUN_AT": "0", "QI_DQ_MARGIN": "0", "QI_DQ_SHIFT": "0"}],
-                         ids=["default", "root", "tinyqueue", "eager"])
-@pytest.mark.parametrize("name", ["tiered_6", "broken", "planted_5_96", "tiered_5_shuffled", "random_28",
-                                  "two_tier_7_256", "correct"])
-def test_persistent_launch_exact(name, env, monkeypatch):
-    monkeypatch.setenv("QI_DONATE", "1")
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    text = _text_for(name)
-    r = GOLD[name] if name in GOLD else Oracle().load(text).solve()
-    d = qa.FBAS(text).solve_stats(jit=2)  # the persistent code is in the specialised kernel only
-    _cmp(d, r, name)
-
-
-def test_persistent_launch_bench_workloads_exact(monkeypatch):
-    monkeypatch.setenv("QI_DONATE", "1")
-    texts = {"two_tier_10_256": fbas_gen.two_tier(10, 256), "two_tier_8_192": fbas_gen.two_tier(8, 192),
-             "planted_deep_8_512": fbas_gen.planted_deep(8, 512)}
-    for name, text in texts.items():
-        d = qa.FBAS(text).solve_stats(jit=2)
-        g = BIG[name]
-        assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (g["verdict"], g["nodes"], g["evals"], g["minq"]), name
-        if "q1" in g:
-            assert (d["q1"], d["q2"]) == (g["q1"], g["q2"]), name
-
-
 # ---- sharded search inside the library (qi_solve_opts.engines / device_mask) ---------------
 # The same code path as a multi-GPU solve: engine 0 grows, every engine keeps its dealt
 # share, engines run chains on their own host threads and streams, best keys and surplus
