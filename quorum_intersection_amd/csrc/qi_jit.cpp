@@ -66,6 +66,139 @@ bool jit_eligible(const LocalFlat& f) {
   return f.T <= 1024 && f.G <= 1024 && f.extra_src.size() <= 4096 && f.grp_extra.size() <= 4096 * 8;
 }
 
+namespace {
+
+// Sibling threshold nodes evaluated bit-sliced.  Leaf TNs (validators only, multiplicity 1)
+// whose vertex masks are the same bit pattern at different positions of one mask word and
+// whose thresholds agree -- the organisations of a tiered FBAS, "2 of 3" each -- are
+// evaluated together: plane j = X >> o_j holds the j-th member of every sibling at the
+// sibling's base bit, a bit-sliced adder counts the planes, and one boolean function of the
+// count bits gives "count >= threshold" for all siblings at once (result bit = base bit).
+// 10 siblings of 3 validators cost 2 shifts + 1 three-input bit operation + 1 AND instead of
+// 10 x (AND, BCNT, compare, select).  Parents count satisfied siblings with one popcount.
+struct SlicedGroup {
+  uint32_t word = 0;              // vertex mask word the siblings live in
+  std::vector<uint32_t> offs;     // bit offsets of the pattern (offs[0] == 0)
+  int32_t t0 = 0, t1 = 0;         // thresholds (outside unavailable / available)
+  std::vector<uint32_t> tns;      // member TNs
+  uint32_t base_bits = 0;         // OR of 1 << base over the members
+};
+
+// Statements that leave in `out` the bitwise "at least k of the planes x[] are set".
+std::string sliced_at_least(const std::vector<std::string>& x, int k, const std::string& out, const std::string& pfx) {
+  const int n = (int)x.size();
+  std::ostringstream o;
+  auto join = [&](const char* op) {
+    std::string e = x[0];
+    for (int i = 1; i < n; ++i) e += std::string(" ") + op + " " + x[i];
+    return e;
+  };
+  if (k <= 0) { o << "const uint32_t " << out << " = 0xFFFFFFFFu;"; return o.str(); }
+  if (k > n) { o << "const uint32_t " << out << " = 0u;"; return o.str(); }
+  if (k == 1) { o << "const uint32_t " << out << " = " << join("|") << ";"; return o.str(); }
+  if (k == n) { o << "const uint32_t " << out << " = " << join("&") << ";"; return o.str(); }
+  if (n == 3) {  // k == 2: majority
+    o << "const uint32_t " << out << " = (" << x[0] << " & " << x[1] << ") | (" << x[2] << " & (" << x[0] << " | " << x[1] << "));";
+    return o.str();
+  }
+  // column compression with full / half adders: cols[w] = bits of weight 2^w
+  std::vector<std::vector<std::string>> cols(4);
+  cols[0] = x;
+  int tmp = 0;
+  for (int w = 0; w < 3; ++w) {
+    while (cols[w].size() > 1) {
+      const std::string s_ = pfx + "s" + std::to_string(tmp), c_ = pfx + "c" + std::to_string(tmp);
+      ++tmp;
+      if (cols[w].size() >= 3) {
+        const std::string a = cols[w][0], b = cols[w][1], c = cols[w][2];
+        cols[w].erase(cols[w].begin(), cols[w].begin() + 3);
+        o << "const uint32_t " << s_ << " = " << a << " ^ " << b << " ^ " << c << "; const uint32_t " << c_ << " = (" << a
+          << " & " << b << ") | (" << c << " & (" << a << " | " << b << ")); ";
+      } else {
+        const std::string a = cols[w][0], b = cols[w][1];
+        cols[w].erase(cols[w].begin(), cols[w].begin() + 2);
+        o << "const uint32_t " << s_ << " = " << a << " ^ " << b << "; const uint32_t " << c_ << " = " << a << " & " << b
+          << "; ";
+      }
+      cols[w].push_back(s_);
+      cols[w + 1].push_back(c_);
+    }
+  }
+  auto bit = [&](int w) -> std::string { return cols[w].empty() ? std::string("0u") : cols[w][0]; };
+  const std::string b0 = bit(0), b1 = bit(1), b2 = bit(2);
+  std::string e;
+  switch (k) {  // count = 4*b2 + 2*b1 + b0 (n <= 7)
+    case 2: e = b1 + " | " + b2; break;
+    case 3: e = "(" + b1 + " & " + b0 + ") | " + b2; break;
+    case 4: e = b2; break;
+    case 5: e = b2 + " & (" + b1 + " | " + b0 + ")"; break;
+    case 6: e = b2 + " & " + b1; break;
+    default: e = b2 + " & " + b1 + " & " + b0; break;  // 7
+  }
+  o << "const uint32_t " << out << " = " << e << ";";
+  return o.str();
+}
+
+std::vector<SlicedGroup> find_sliced_groups(const LocalFlat& f, std::vector<int>& grp_of, std::vector<uint32_t>& base_of) {
+  grp_of.assign(f.T, -1);
+  base_of.assign(f.T, 0);
+  std::vector<SlicedGroup> groups;
+  if (std::getenv("QI_JIT_NO_SLICE")) return groups;  // diagnostics: per-TN evaluation only
+  for (uint32_t t = 0; t < f.T; ++t) {
+    if (f.flags[t] & 3u) continue;  // inverted test or extra multiplicity planes
+    bool leaf = true;
+    for (uint32_t w = 0; w < f.tw; ++w) leaf = leaf && f.cmask[(size_t)t * f.tw + w] == 0;
+    if (!leaf || f.extra_off[t] != f.extra_off[t + 1]) continue;
+    int word = -1;
+    bool one = true;
+    for (uint32_t w = 0; w < f.mw; ++w)
+      if (f.vmask[(size_t)t * f.mw + w]) {
+        one = one && word < 0;
+        word = (int)w;
+      }
+    if (word < 0 || !one) continue;
+    const uint32_t m = f.vmask[(size_t)t * f.mw + word];
+    const int n = __builtin_popcount(m);
+    const int32_t t0 = f.thr[2 * t], t1 = f.thr[2 * t + 1];
+    if (n > 7 || t0 < 1 || t0 > n || t1 < 1 || t1 > n) continue;
+    const uint32_t base = (uint32_t)__builtin_ctz(m);
+    std::vector<uint32_t> offs;
+    for (uint32_t b = base; b < 32; ++b)
+      if ((m >> b) & 1u) offs.push_back(b - base);
+    int g = -1;
+    for (size_t i = 0; i < groups.size(); ++i)
+      if (groups[i].word == (uint32_t)word && groups[i].offs == offs && groups[i].t0 == t0 && groups[i].t1 == t1 &&
+          !((groups[i].base_bits >> base) & 1u))
+        g = (int)i;
+    if (g < 0) {
+      SlicedGroup ng;
+      ng.word = (uint32_t)word;
+      ng.offs = offs;
+      ng.t0 = t0;
+      ng.t1 = t1;
+      groups.push_back(ng);
+      g = (int)groups.size() - 1;
+    }
+    groups[g].tns.push_back(t);
+    groups[g].base_bits |= 1u << base;
+    grp_of[t] = g;
+    base_of[t] = base;
+  }
+  // a group pays off from three siblings on; smaller ones stay per-TN
+  std::vector<SlicedGroup> kept;
+  std::vector<int> remap(groups.size(), -1);
+  for (size_t i = 0; i < groups.size(); ++i)
+    if (groups[i].tns.size() >= 3) {
+      remap[i] = (int)kept.size();
+      kept.push_back(groups[i]);
+    }
+  for (uint32_t t = 0; t < f.T; ++t)
+    if (grp_of[t] >= 0) grp_of[t] = remap[grp_of[t]];
+  return kept;
+}
+
+}  // namespace
+
 std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps) {
   std::ostringstream o;
   if (stamps) o << "#define QI_STAMPS 1\n";
@@ -101,15 +234,62 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   for (int w = 1; w < MW; ++w) o << " | X[" << w << "]";
   o << ")) return false;\n      ++rounds;\n";
   for (int w = 0; w < TW; ++w) o << "      uint32_t sb" << w << " = 0u;\n";
+  // sibling groups first (leaf TNs): R<g> bit `base` = sibling satisfied
+  std::vector<int> grp_of;
+  std::vector<uint32_t> base_of;
+  const std::vector<SlicedGroup> sgroups = find_sliced_groups(f, grp_of, base_of);
+  for (size_t g = 0; g < sgroups.size(); ++g) {
+    const SlicedGroup& sg = sgroups[g];
+    const std::string G = std::to_string(g);
+    std::vector<std::string> planes;
+    o << "      uint32_t R" << G << ";\n      {";
+    for (size_t j = 0; j < sg.offs.size(); ++j) {
+      const std::string nm = "p" + G + "_" + std::to_string(j);
+      if (sg.offs[j] == 0) o << " const uint32_t " << nm << " = X[" << sg.word << "];";
+      else o << " const uint32_t " << nm << " = X[" << sg.word << "] >> " << sg.offs[j] << "u;";
+      planes.push_back(nm);
+    }
+    o << "\n        " << sliced_at_least(planes, sg.t0, "ge0_", "a" + G + "_") << "\n";
+    if (sg.t1 != sg.t0) {
+      o << "        " << sliced_at_least(planes, sg.t1, "ge1_", "b" + G + "_") << "\n";
+      o << "        R" << G << " = (POL == 0 ? ge0_ : POL == 1 ? ge1_ : (pol ? ge1_ : ge0_)) & " << hex(sg.base_bits) << "; }\n";
+    } else {
+      o << "        R" << G << " = ge0_ & " << hex(sg.base_bits) << "; }\n";
+    }
+  }
+  // popcount terms of a mask over TN-satisfaction word w: grouped children are counted in
+  // their group's result word, the rest in sb<w>
+  auto child_terms = [&](uint32_t w, uint32_t m, std::vector<std::string>& terms) {
+    uint32_t rest = m;
+    std::vector<uint32_t> sub(sgroups.size(), 0);
+    for (uint32_t b = 0; b < 32; ++b) {
+      const uint32_t c = 32 * w + b;
+      if (((m >> b) & 1u) && c < f.T && grp_of[c] >= 0) {
+        rest &= ~(1u << b);
+        sub[grp_of[c]] |= 1u << base_of[c];
+      }
+    }
+    if (rest) terms.push_back("__popc(sb" + std::to_string(w) + " & " + hex(rest) + ")");
+    for (size_t g = 0; g < sgroups.size(); ++g)
+      if (sub[g]) {
+        if (sub[g] == sgroups[g].base_bits) terms.push_back("__popc(R" + std::to_string(g) + ")");
+        else terms.push_back("__popc(R" + std::to_string(g) + " & " + hex(sub[g]) + ")");
+      }
+  };
+  // 0/1 satisfaction of TN t as an expression
+  auto sat_bit = [&](uint32_t t) -> std::string {
+    if (grp_of[t] >= 0) return "((R" + std::to_string(grp_of[t]) + " >> " + std::to_string(base_of[t]) + "u) & 1u)";
+    return "((sb" + std::to_string(t / 32) + " >> " + std::to_string(t % 32) + "u) & 1u)";
+  };
   std::vector<std::vector<std::string>> extra(f.T);
   for (uint32_t t = 0; t < f.T; ++t)
     for (uint32_t e = f.extra_off[t]; e < f.extra_off[t + 1]; ++e) {
       const uint32_t src = f.extra_src[e];
-      const std::string m = hex(f.extra_mask[e]);
-      if (src < f.mw) extra[t].push_back("__popc(X[" + std::to_string(src) + "] & " + m + ")");
-      else extra[t].push_back("__popc(sb" + std::to_string(src - f.mw) + " & " + m + ")");
+      if (src < f.mw) extra[t].push_back("__popc(X[" + std::to_string(src) + "] & " + hex(f.extra_mask[e]) + ")");
+      else child_terms(src - f.mw, f.extra_mask[e], extra[t]);
     }
   for (uint32_t t = 0; t < f.T; ++t) {
+    if (grp_of[t] >= 0) continue;  // evaluated with its siblings above
     std::vector<std::string> terms;
     for (uint32_t w = 0; w < f.mw; ++w) {
       const uint32_t m = f.vmask[(size_t)t * f.mw + w];
@@ -117,7 +297,7 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
     }
     for (uint32_t w = 0; w < f.tw; ++w) {
       const uint32_t m = f.cmask[(size_t)t * f.tw + w];
-      if (m) terms.push_back("__popc(sb" + std::to_string(w) + " & " + hex(m) + ")");
+      if (m) child_terms(w, m, terms);
     }
     for (auto& x : extra[t]) terms.push_back(x);
     std::string c = terms.empty() ? std::string("0u") : terms[0];
@@ -149,14 +329,14 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   }
   if (one_root) {
     const uint32_t tn = f.root_tn[0];
-    o << "#if QI_ONE_ROOT\n      { const bool s_ = (sb" << (tn / 32) << " >> " << (tn % 32) << "u) & 1u; if (!s_) {";
+    o << "#if QI_ONE_ROOT\n      { const bool s_ = " << sat_bit(tn) << " != 0u; if (!s_) {";
     for (int w = 0; w < MW; ++w) o << " X[" << w << "] = 0u;";
     o << " } return s_; }\n#endif\n";
   }
   for (int w = 0; w < MW; ++w) o << "      uint32_t n" << w << " = 0u;\n";
   for (uint32_t r = 0; r < f.R; ++r) {
     const uint32_t tn = f.root_tn[r];
-    o << "      { const uint32_t s = 0u - ((sb" << (tn / 32) << " >> " << (tn % 32) << "u) & 1u);";
+    o << "      { const uint32_t s = 0u - " << sat_bit(tn) << ";";
     for (uint32_t w = 0; w < f.mw; ++w) {
       const uint32_t u = f.root_users[(size_t)r * f.mw + w];
       if (u) o << " n" << w << " |= " << hex(u) << " & s;";

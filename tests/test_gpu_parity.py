@@ -624,6 +624,26 @@ def test_large_scc_beyond_256(k, n):
     _validate_witness(text, d["q1"], d["q2"])
 
 
+def _flat_fbas(n, thr):
+    ids = [f"V{i:03d}" for i in range(n)]
+    return json.dumps([{"publicKey": k, "name": k.lower(),
+                        "quorumSet": {"threshold": thr, "validators": ids, "innerQuorumSets": []}} for k in ids])
+
+
+@pytest.mark.parametrize("n,engines", [(300, 1), (300, 3), (520, 1)])
+def test_large_scc_witness_deeper_than_256_levels(n, engines):
+    # One SCC of n > 256 vertices where any two vertices form a quorum: the exclusion-first
+    # descent drops n - 2 vertices before the first minimal quorum, so the witness (and the
+    # records before it) lie ~n levels deep and their path keys use more than 8 words.
+    # Pruning and the preorder-filtered totals compare whole keys (10 / 17 words here).
+    text = _flat_fbas(n, 2)
+    r = Oracle().load(text).solve()
+    assert len(r["front"]) == n and not r["verdict"] and r["nodes"] > n
+    d = qa.FBAS(text).solve_stats(engines=engines, device_mask=1 if engines > 1 else 0)
+    _cmp(d, r, f"flat_{n}")
+    _validate_witness(text, d["q1"], d["q2"])
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_gfp_batch_global_scratch(seed, monkeypatch):
     # networks whose per-query image exceeds the LDS run the batched kernel on global
