@@ -624,6 +624,44 @@ def test_large_scc_beyond_256(k, n):
     _validate_witness(text, d["q1"], d["q2"])
 
 
+def _org_tier_fbas(sizes, thr_in, thr_out, partial=False):
+    """One SCC of organisations of the given sizes; every validator's quorum set is thr_out of
+    the organisations' inner sets (thr_in of the organisation's validators).  partial: each
+    validator leaves one organisation out (parents then count subsets of a sibling group)."""
+    orgs, vid = [], 0
+    for sz in sizes:
+        orgs.append([f"T{vid + i:02d}" for i in range(sz)])
+        vid += sz
+    tin = thr_in if isinstance(thr_in, list) else [thr_in] * len(sizes)
+    nodes = []
+    for i, o in enumerate(orgs):
+        for k in o:
+            inner = [{"threshold": tin[j], "validators": orgs[j], "innerQuorumSets": []}
+                     for j in range(len(sizes)) if not (partial and (j + i) % len(sizes) == len(sizes) - 1)]
+            nodes.append({"publicKey": k, "name": k, "quorumSet": {"threshold": thr_out - (1 if partial else 0),
+                                                                   "validators": [], "innerQuorumSets": inner}})
+    return json.dumps(nodes)
+
+
+@pytest.mark.parametrize("cfg", [([4] * 4, 3, 3, False), ([5] * 4, 3, 3, False), ([7] * 3, 6, 2, False),
+                                 ([4] * 6, 4, 4, False), ([3] * 6, 2, 4, True), ([6] * 4, 4, 3, False),
+                                 ([3, 3, 3, 5, 5, 5], [2, 2, 2, 4, 4, 4], 5, False), ([3, 3, 3, 6, 6, 6], [3, 3, 3, 5, 5, 5], 4, False),
+                                 ([4, 4, 4, 6, 6, 6], [2, 3, 2, 5, 4, 5], 4, True),
+                                 ([7] * 4, 7, 3, False), ([2] * 9, 1, 6, False), ([5] * 5, 5, 4, True)],
+                         ids=lambda c: "x".join(map(str, c[0])) + f"_{c[1]}_{c[2]}_{int(c[3])}".replace(" ", ""))
+def test_sibling_groups_bit_sliced_exact(cfg):
+    # organisations of 2-7 validators with thresholds 1..n: the specialised kernel evaluates
+    # equal-shaped sibling threshold nodes bit-sliced (adders over vertex planes); the
+    # table-interpreting kernel and the oracle count them one by one
+    text = _org_tier_fbas(*cfg)
+    r = Oracle().load(text).solve()
+    for jit in (2, 1):
+        d = qa.FBAS(text).solve_stats(jit=jit)
+        _cmp(d, r, str(cfg))
+    if not d["verdict"] and d["searched"]:
+        _validate_witness(text, d["q1"], d["q2"])
+
+
 def _flat_fbas(n, thr):
     ids = [f"V{i:03d}" for i in range(n)]
     return json.dumps([{"publicKey": k, "name": k.lower(),
