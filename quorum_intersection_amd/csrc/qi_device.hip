@@ -608,6 +608,11 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
     jit_smax_ = SMAX;
+    // |SCC| <= 32: 20 stack levels leave LDS for 9 resident waves per CU instead of 8
+    // (17,408 B per wave).  Measured on the bench workload: 24 / 22 / 21 / 20 / 19 / 14 levels
+    // = 8 / 8 / 8 / 9 / 9 / 12 waves gave 2.63 / 2.62 / 2.55 / 2.39 / 2.38 / 2.48 ms; below 19
+    // the extra stack evictions cost more than the waves bring.
+    if (MW == 1 && !ORD) jit_smax_ = 20;
     if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
     if (ORD) cfg_.jit = 1;  // no run-time specialisation of the ordered kernel
     stream_ = acquire_stream(device_);

@@ -387,19 +387,57 @@ constexpr int search_lds_words() {
 // Diagnostic build only (QI_STAMPS, run-time specialised kernel with jit=3): per-wave
 // s_memtime sums of the loop sections, added into totals[8..15].  The production kernels
 // contain no stamps.
+// Loop sections (fine ids) and the six buckets a stamp build reports them in
+// (QI_STAMP_SET: 0 = everything, coarse; 1 and 2 = two fine views; -1 = not recorded).
+enum : int { F_POP = 0, F_INSTALL, F_POLL, F_SPILL, F_GFP1, F_GFP2, F_BEST, F_PUSH, F_FLUSH, F_CLAIM, F_FASTP, F_FASTMIN,
+             F_COOP, F_W_INSTALL, F_W_CLAIM, F_W_POP, F_RESET, F_FAST };
+#ifndef QI_STAMP_SET
+#define QI_STAMP_SET 0
+#endif
+constexpr int stamp_bucket(int f) {
+  if (QI_STAMP_SET == 1)
+    return f == F_POP ? 0 : f == F_INSTALL ? 1 : f == F_BEST ? 2 : f == F_PUSH ? 3 : f == F_FLUSH ? 4 : f == F_CLAIM ? 5 : -1;
+  if (QI_STAMP_SET == 4)  // fast steps against everything else
+    return f == F_FAST ? 0 : 1;
+  if (QI_STAMP_SET == 3)  // explicit waits only: unit loads at install, vmcnt drain at claim, LDS refill at pop
+    return f == F_W_INSTALL ? 0 : f == F_W_CLAIM ? 1 : f == F_W_POP ? 2 : -1;
+  if (QI_STAMP_SET == 2)
+    return f == F_FASTP ? 0 : f == F_FASTMIN ? 1 : f == F_COOP ? 2 : f == F_POLL ? 3 : f == F_SPILL ? 4
+           : (f == F_GFP1 || f == F_GFP2) ? 5 : -1;
+  return f == F_FAST ? 2 : f <= F_INSTALL ? 0 : f == F_POLL ? 1 : f == F_SPILL ? 2 : f <= F_GFP2 ? 3 : f <= F_CLAIM ? 4 : 5;
+}
 #ifdef QI_STAMPS
 #define QI_STAMP(slot)                                                   \
   do {                                                                   \
     __builtin_amdgcn_sched_barrier(0);                                   \
     const uint64_t now_ = __builtin_amdgcn_s_memtime();                  \
     __builtin_amdgcn_sched_barrier(0);                                   \
-    stamp_sum[(slot)] += now_ - stamp_prev;                              \
+    if (stamp_bucket(slot) >= 0) stamp_sum[stamp_bucket(slot) < 0 ? 0 : stamp_bucket(slot)] += now_ - stamp_prev; \
     stamp_prev = now_;                                                   \
   } while (0)
+// stamp set 3: an explicit counter wait bracketed by stamps (what the wave waits there)
+#if QI_STAMP_SET == 3
+#define QI_WAIT_STAMP(what, id)                 \
+  do {                                          \
+    QI_STAMP(F_RESET);                          \
+    asm volatile("s_waitcnt " what ::: "memory"); \
+    QI_STAMP(id);                               \
+  } while (0)
+#else
+#define QI_WAIT_STAMP(what, id) \
+  do {                          \
+  } while (0)
+#endif
 #elif defined(QI_MARKS)
 // diagnostics: assembly markers at the section boundaries (static instruction counts)
 #define QI_STAMP(slot) asm volatile(";QIMARK " #slot ::: "memory")
+#define QI_WAIT_STAMP(what, id) \
+  do {                          \
+  } while (0)
 #else
+#define QI_WAIT_STAMP(what, id) \
+  do {                          \
+  } while (0)
 #define QI_STAMP(slot) \
   do {                 \
   } while (0)
@@ -417,11 +455,31 @@ constexpr int search_lds_words() {
 #ifndef QI_LDS_OW
 #define QI_LDS_OW 0
 #endif
-// iterations between polls of the global queue head and the device-side best key
-// (32 -> 128 iterations measured 3.45-3.59 -> 3.20-3.24 ms per search on the bench
-// workload and 1.50 -> 1.37 ms on planted_deep; 256/512/1024 slower)
-#ifndef QI_POLL_MASK
-#define QI_POLL_MASK 127
+// Iterations (fast steps included) between polls of the global queue head and the
+// device-side best key.  A wave with an idle lane learns that the queue is dry from its own
+// failed claim; the poll only ends waves whose lanes are all still busy, and ending those
+// early costs more (spilled stacks, extra launches) than it saves: on the bench workload
+// 192 / 256 / 384 / 512 / 1024 iterations gave 2.61 / 2.48 / 2.22 / 2.25 / 2.32 ms.
+#ifndef QI_POLL_EVERY
+#define QI_POLL_EVERY 384
+#endif
+// Fast steps: up to QI_FAST_STEPS lean iterations run between two full ones while at least
+// QI_FAST_MIN lanes can pop or process a node without any service (no unit to install, no
+// quorum leaf, no full stack) and no witness is known (nothing to prune).  The full
+// iteration below carries every rarely needed path; paying for it on every node made the
+// loop issue-bound on control code.
+#ifndef QI_FAST_STEPS
+#define QI_FAST_STEPS 3
+#endif
+#ifndef QI_FAST_MIN
+#define QI_FAST_MIN 56
+#endif
+// claim the next units (and flush records) right after the installs instead of after the push
+#ifndef QI_CLAIM_FIRST
+#define QI_CLAIM_FIRST 0
+#endif
+#ifndef QI_FLUSH_AFTER
+#define QI_FLUSH_AFTER 1
 #endif
 
 template <int MW, int TW, int SMAX, class EV>
@@ -523,7 +581,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   bool must_spill = false;  // an eviction found the pool empty: spill at the next iteration
   uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
   bool dry = false;         // wave-uniform: no unit left to claim (head >= n_in)
-  uint32_t iter = 0;
+  uint32_t iter = 0;        // wave-uniform: iterations so far, fast steps included
+  uint32_t next_poll = 0;   // the poll is due in the first full iteration with iter >= next_poll
+  bool poll_issued = true;  // its loads are in flight (the first ones are issued before the loop)
   // the next unit of this lane: claimed index (= its log record index) + (PREFETCH) its
   // words in registers; installed at the start of the iteration after the lane ran out
   bool fpend = false;
@@ -590,9 +650,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   for (int w = 0; w < RL::WORDS; ++w) rec[w] = 0;
   auto flush_record = [&]() {
     if (rec_pend) {
+#ifndef QI_ABL_NOREC  // diagnostics: no record stores (counts then only via the running totals)
       uint32_t* r = records + (size_t)rec_idx * RL::WORDS;
 #pragma unroll
       for (int w = 0; w < RL::WORDS; ++w) r[w] = rec[w];
+#endif
       rec_pend = false;
     }
   };
@@ -731,6 +793,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       const uint32_t avail = pool_end - pool_next;
       const uint32_t r = rank_in(wm);
       if (want && r < avail) {
+        QI_WAIT_STAMP("vmcnt(0)", F_W_CLAIM);
         fidx = pool_next + r;
         fpend = true;
         want = false;
@@ -746,6 +809,111 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   };
 
   for (;;) {
+#if QI_FAST_STEPS > 0
+    // ---- (0) fast steps: pop or process one node per lane, common outcomes only --------
+    // A lane whose node is a quorum leaf (cpp:281) or whose push would need an eviction is
+    // held, uncommitted, for the full iteration; lanes without node and stack wait there too.
+    // (not in the growth launches: their per-lane node budget is the grow budget exactly)
+    if (budget > 2u * (uint32_t)QI_FAST_STEPS && best64 == ~0ull && !(MW > 1 && a.has_best)) {
+      bool hold = false;
+#pragma unroll 1
+      for (int fs = 0; fs < QI_FAST_STEPS; ++fs) {
+        const bool elig = !done && !hold && (has || tvalid);
+        if ((uint32_t)__popcll(__ballot(elig)) < (uint32_t)QI_FAST_MIN) break;
+        ++wave_iters;
+        ++iter;
+#ifdef QI_DIAG_FAST  // diagnostics: fast steps counted in the cooperative-phase counter
+        ++coop_phases;
+#endif
+        if (elig && !has) {  // pop (no witness known: nothing to prune)
+          const uint32_t b = tpk & 255u, de = (tpk >> 8) & 511u, dle = tpk >> 17;
+          key_prefix_bit<MW>(K, de);
+#pragma unroll
+          for (int w = 0; w < MW; ++w) {
+            T[w] = tT[w];
+            D[w] = tD[w];
+          }
+          set_ord(dle, b);
+          dlen = dle + 1;
+          depth = de + 1;
+          has = true;
+          if (nst > 0) {
+            --nst;
+            const uint32_t pos = spos(nst);
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+              tT[w] = ST_(pos, w);
+              tD[w] = ST_(pos, MW + w);
+            }
+            tpk = ST_(pos, 2 * MW);
+          } else {
+            tvalid = false;
+          }
+        }
+        const bool full = tvalid && nst == (uint32_t)SMAX;  // a push would need an eviction
+        uint32_t any = 0;
+#pragma unroll
+        for (int w = 0; w < MW; ++w) any |= T[w] | D[w];
+        const bool leaf0 = dlen > a.half_m || !any;  // cpp:261 / cpp:266
+        const bool ev = elig && !full && !leaf0;
+        uint32_t X[MW];
+#pragma unroll
+        for (int w = 0; w < MW; ++w) X[w] = ev ? D[w] : 0u;
+        const uint32_t r0 = rounds;
+        const bool dq = EV::template gfp<0>(f, X, 0u, rounds);  // cpp:281
+        if (dq) rounds = r0;  // re-evaluated (and counted) by the full iteration
+        hold = hold || (elig && (full || dq));
+        const bool go = elig && !full && !dq;  // this lane commits its node in this step
+        const bool ev2 = go && !leaf0;
+#pragma unroll
+        for (int w = 0; w < MW; ++w) X[w] = ev2 ? (T[w] | D[w]) : 0u;
+        const bool qne = EV::template gfp<0>(f, X, 0u, rounds);  // cpp:301
+        if (go) {
+          ++steps;
+          ++seg_count;
+          if (leaf0) has = false;
+        }
+        if (ev2) {
+          seg_evals += 2u;
+          uint32_t dout = 0, qd = 0;
+#pragma unroll
+          for (int w = 0; w < MW; ++w) {
+            dout |= D[w] & ~X[w];
+            qd |= X[w] & ~D[w];
+          }
+          if (!qne || dout || !qd) {  // cpp:303, 308-314, 325
+            has = false;
+          } else {
+            const uint32_t pb = EV::best(f, X, D, seg_zfb);  // cpp:317
+#pragma unroll
+            for (int w = 0; w < MW; ++w) X[w] &= ~D[w];
+            X[pb >> 5] &= ~(1u << (pb & 31u));  // toRemove' = Q \ D \ {b} (cpp:330-334)
+            if (tvalid) {  // the old top goes to LDS (room checked above)
+              const uint32_t pos = spos(nst);
+#pragma unroll
+              for (int w = 0; w < MW; ++w) {
+                ST_(pos, w) = tT[w];
+                ST_(pos, MW + w) = tD[w];
+              }
+              ST_(pos, 2 * MW) = tpk;
+              ++nst;
+            }
+#pragma unroll
+            for (int w = 0; w < MW; ++w) {
+              tT[w] = X[w];
+              tD[w] = D[w];
+              T[w] = X[w];
+            }
+            tD[pb >> 5] |= 1u << (pb & 31u);
+            tpk = pb | (depth << 8) | (dlen << 17);
+            tvalid = true;
+            ++depth;  // continue with the exclusion branch (cpp:336)
+          }
+        }
+      }
+    }
+    QI_STAMP(F_FAST);
+#endif
     // ---- (1) lanes without a node: pop the top of stack, else install the next unit ----
     if (!done && !has) {
       if (tvalid) {
@@ -777,14 +945,17 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
               tD[w] = ST_(pos, MW + w);
             }
             tpk = ST_(pos, 2 * MW);
+            QI_WAIT_STAMP("lgkmcnt(0)", F_W_POP);
           } else {
             tvalid = false;
           }
         }
       }
+      QI_STAMP(F_POP);
       if (!has) {
         if (seg_open) close_segment();  // the unit's subtree is done
         if (fpend && steps < limit) {  // install the claimed unit
+          QI_WAIT_STAMP("vmcnt(0)", F_W_INSTALL);
           uint32_t UK[MW];
 #pragma unroll
           for (int w = 0; w < MW; ++w) {
@@ -819,21 +990,30 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
-    QI_STAMP(0);  // pop / install
+    QI_STAMP(F_INSTALL);
+#if QI_CLAIM_FIRST
+    // Claim right after the installs: a lane that now holds only its node (or nothing) will
+    // need a unit next, and the unit's loads get this whole iteration to land.  vmcnt
+    // counts loads and stores in issue order and the compiler drains it before the claim's
+    // loads (their destination registers are loop-carried): here that drain finds only
+    // operations a full iteration old, and the record stores follow the loads.
+    claim();
+    QI_STAMP(F_CLAIM);
+    flush_record();
+    QI_STAMP(F_FLUSH);
+#endif
     // a lane with nothing left is done once it cannot get a unit any more (a claimed unit
     // past the budget is spilled below)
     if (!has && !tvalid && nst == 0 && !fpend && (steps >= limit || pool_dead)) done = true;
 
-    // Every QI_POLL_MASK + 1 iterations poll the global head and the device-side best key
-    // (loads issued one iteration ahead).  Once no unit is left to claim anywhere, every
+    // Every QI_POLL_EVERY iterations poll the global head and the device-side best key
+    // (loads issued one full iteration ahead).  Once no unit is left to claim anywhere, every
     // lane gets a short grace period and then spills: the next launch spreads the
     // remaining subtrees over all lanes instead of letting a few lanes grind through deep
     // subtrees while the rest idle.
-    if (((iter + 1u) & (uint32_t)QI_POLL_MASK) == 0u && lane == 0) {
-      poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      poll_b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if ((iter++ & (uint32_t)QI_POLL_MASK) == 0u) {
+    if (poll_issued && iter >= next_poll) {
+      poll_issued = false;
+      next_poll = iter + (uint32_t)QI_POLL_EVERY;
       uint32_t h = 0;
       uint64_t b = ~0ull;
       if (lane == 0) {
@@ -846,9 +1026,17 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         dry = true;
         limit = min(limit, steps + a.grace);
       }
+    } else if (!poll_issued && iter + 2u * ((uint32_t)QI_FAST_STEPS + 1u) >= next_poll) {
+      // at least one full iteration before the poll that reads them
+      poll_issued = true;
+      if (lane == 0) {
+        poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        poll_b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+    ++iter;
 
-    QI_STAMP(1);  // polls
+    QI_STAMP(F_POLL);
     // ---- (3) budget exhausted: spill current node, top, stack and claimed unit ---------
     {
       const bool spill = (has && (steps >= limit || must_spill)) || (!has && fpend && steps >= limit);
@@ -872,7 +1060,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     }
     if (!__any(!done)) break;
 
-    QI_STAMP(2);  // spill
+    QI_STAMP(F_SPILL);
     // ---- (4) one search node per active lane (cpp:258-345) ---------------------------
     ++wave_iters;
     bool pending = false;
@@ -897,10 +1085,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       pending = dq;
     }
     const bool active2 = active && !dq;
+    QI_STAMP(F_GFP1);
 #pragma unroll
     for (int w = 0; w < MW; ++w) X[w] = active2 ? (T[w] | D[w]) : 0u;
     const bool qne = EV::template gfp<0>(f, X, 0u, rounds);  // cpp:301
-    QI_STAMP(3);  // the two fixpoints
+    QI_STAMP(F_GFP2);
     bool push = false;
     uint32_t pb = 0;
     if (active2) {
@@ -921,6 +1110,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         push = true;
       }
     }
+    QI_STAMP(F_BEST);
     // push the inclusion branch (cpp:343-345): the old top goes to LDS (a full stack
     // first evicts its shallowest entry into the next frontier; wave-aggregated slot
     // reservation, convergent), the new entry becomes the top.  Then continue with the
@@ -973,9 +1163,20 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 
     // the unit loads of lanes that became free: in flight during the quorum-leaf phase
     // below (the install waits on vmcnt, which counts stores and loads in issue order)
-    flush_record();
+    QI_STAMP(F_PUSH);
+#if !QI_CLAIM_FIRST
+#if QI_FLUSH_AFTER
     claim();
-    QI_STAMP(4);  // findBestNode + push
+    QI_STAMP(F_CLAIM);
+    flush_record();
+    QI_STAMP(F_FLUSH);
+#else
+    flush_record();
+    QI_STAMP(F_FLUSH);
+    claim();
+    QI_STAMP(F_CLAIM);
+#endif
+#endif
     // ---- (5) quorum leaves: isMinimalQuorum + visitor ---------------------------------
     // Quorum leaves with |D| - 1 < qmin: no D \ {v} can hold a quorum (LocalFlat::qmin),
     // so D is minimal without evaluating them (still credited, as the reference makes the
@@ -997,6 +1198,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
     }
+    QI_STAMP(F_FASTP);
 #if QI_FASTMIN
     // Quorum leaves with |D| = qmin + 1: every D \ {v} has qmin vertices, so it holds a
     // quorum iff it is a fixpoint itself, which one removal-sensitivity pass decides for
@@ -1066,6 +1268,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // (l / S) of the current pass, job k = l % S (+ chunk offset when |D|+1 > S).  The
     // owner's D, lane and |D| arrive through an LDS slot, results by one LDS ds_or per
     // successful job.
+    QI_STAMP(F_FASTMIN);
     const uint64_t pm = __ballot(pending);
     if (pm) {
       ++coop_phases;
@@ -1139,10 +1342,12 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
       __syncthreads();
+#if !QI_CLAIM_FIRST
       flush_record();  // lanes freed by the cooperative phase
       claim();
+#endif
     }
-    QI_STAMP(5);  // quorum-leaf phase
+    QI_STAMP(F_COOP);
   }
   flush_record();
 

@@ -125,6 +125,7 @@ class DeviceSearch(SearchBackend):
         self.dispatches += int(info.dispatches)
         self.dispatch_ms += info.dispatch_ms
         self.spec_launches = getattr(self, "spec_launches", 0) + int(info.specialized)
+        self.blocks = int(info.blocks)
 
     def grow(self, target):
         info = self._c.StepInfo()

@@ -18,12 +18,21 @@ distributed_search(be, device="cuda")
 loc = be.reduce(None)
 st = loc["stamps"][:6]
 tot = sum(st)
-names = ["pop/close", "fetch+poll", "spill", "fixpoints", "best+push", "coop"]
+SETS = {0: ["pop+install", "poll", "spill", "fixpoints", "best+push+flush+claim", "leaf phases"],
+        1: ["pop", "close+install", "dout/qd+best", "evict+push", "flush_record", "claim"],
+        4: ["fast steps", "full iterations", "-", "-", "-", "-"],
+        3: ["install: vmcnt(0) wait", "claim: vmcnt(0) drain", "pop: LDS refill wait", "-", "-", "-"],
+        2: ["fastp (|D|<=qmin)", "fastmin (|D|=qmin+1)", "coop (|D|>=qmin+2)", "done+poll", "spill", "fixpoints"]}
+sset = 0
+for tok in os.environ.get("QI_JIT_DEFINES", "").split(","):
+    if tok.startswith("QI_STAMP_SET="):
+        sset = int(tok.split("=")[1])
+names = SETS[sset]
 waves = max(loc["stamps"][7], 1)
 life_s = loc["stamps"][6] * 1e-8  # summed wave lifetimes
 kernel_s = be.kernel_ms * 1e-3
 cus = torch.cuda.get_device_properties(0).multi_processor_count
-print(json.dumps({"nodes": loc["nodes"], "wave_iters": loc["wave_iters"], "coop_phases": loc["coop_phases"],
+print(json.dumps({"stamp_set": sset, "nodes": loc["nodes"], "wave_iters": loc["wave_iters"], "coop_phases": loc["coop_phases"], "stamp_cycles": st,
                   "cycles_per_wave_iter": tot / max(loc["wave_iters"], 1),
                   "share": {n: round(v / tot, 4) for n, v in zip(names, st)},
                   "cycles_per_iter": {n: round(v / max(loc["wave_iters"], 1), 1) for n, v in zip(names, st)},
