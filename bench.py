@@ -132,7 +132,7 @@ def main():
 
     import quorum_intersection_amd as qa
     from quorum_intersection_amd import fbas_gen
-    from quorum_intersection_amd.distributed import DeviceSearch, distributed_search
+    from quorum_intersection_amd.distributed import DeviceSearch, SharedBest, distributed_search
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -165,6 +165,10 @@ def main():
 
     fb = qa.FBAS(text, device=gpu)
     be = DeviceSearch(fb, args.grow_budget, args.run_budget, args.max_blocks, jit=args.jit, batch=batch)
+    # N > 1: the ranks' shared best-witness key (early termination inside a chain)
+    shared = SharedBest.for_group(tag=os.environ.get("MASTER_PORT", "0")) if world > 1 else None
+    if shared is not None:
+        be.share_best(shared)
 
     # ---- time-to-verdict from JSON text (host parse + flatten + upload + solve), N=1 path,
     # with the CLI's policy: the specialised kernel from the on-disk cache (filled above)
@@ -177,7 +181,7 @@ def main():
 
     def one_step():
         fb.gfp_batch(scc_masks, scc_masks)          # per-SCC checks (cpp:649-672)
-        return distributed_search(be, device=comm_dev, seed_units=args.seed_units)  # search (cpp:691 -> 348-400)
+        return distributed_search(be, device=comm_dev, seed_units=args.seed_units, shared=shared)  # cpp:691 -> 348-400
 
     for _ in range(args.warmup):
         one_step()
@@ -241,6 +245,10 @@ def main():
         except Exception:
             traffic = None
 
+    if shared is not None:
+        be.share_best(None)
+        dist.barrier()
+        shared.close()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define QI_ABI_VERSION 3
+#define QI_ABI_VERSION 4
 
 enum {
   QI_OK = 0,
@@ -146,6 +146,8 @@ typedef struct {
   uint32_t devices;        /* distinct HIP devices they ran on */
   uint64_t units_moved;    /* frontier units handed between shards (rebalancing) */
   double t_device_init_ms; /* HIP runtime / device contexts of the search devices, host wall */
+  uint64_t nodes_processed; /* search nodes the engines ran; > nodes when work after the first
+                               witness in preorder was done before the witness was known */
 } qi_solve_result;
 
 /* q1, q2: caller buffers of n_vertices entries (may be NULL).  q1 = disjoint quorum
@@ -238,6 +240,16 @@ int qi_search_import(qi_search* s, uint64_t count, const void* device_src);
 /* Best witness found locally: key[key_words], depth; returns 1 if any. */
 int qi_search_local_best(qi_search* s, uint32_t* key, uint32_t* depth);
 int qi_search_set_best(qi_search* s, const uint32_t* key, uint32_t depth);
+/* Early termination across cooperating searches inside a chain of launches (the reference
+ * stops the whole search at the first disjoint pair, cpp:369-377).  host_word: 8 bytes of
+ * host memory, 8-byte aligned, shared by every qi_search working on the same search (in one
+ * process, or mapped into several, e.g. a POSIX shared-memory page on one node); all ones =
+ * no witness.  After every launch a search folds its best key into the word (atomic
+ * minimum) and its kernels poll it, so a witness found on one GPU prunes the others within
+ * a few launches; qi_search_local_best / qi_search_set_best / qi_search_reduce still decide
+ * the exact result.  The library pins the page if it is not HIP host memory.  The caller
+ * writes all ones before a new search; NULL ends the sharing. */
+int qi_search_share_best(qi_search* s, void* host_word);
 /* Sums over processed segments at or before (key, depth) in preorder; key NULL = all. */
 int qi_search_reduce(qi_search* s, const uint32_t* key, uint32_t depth, qi_totals* out);
 /* Witness of the local best: q1 (scc order) / q2 (branch order), global indices. */

@@ -58,6 +58,7 @@ class SolveResult(ctypes.Structure):
         ("devices", c_uint32),
         ("units_moved", c_uint64),
         ("t_device_init_ms", c_double),
+        ("nodes_processed", c_uint64),
     ]
 
 
@@ -131,6 +132,7 @@ SIGNATURES = {
     "qi_search_import": (c_int, [c_void_p, c_uint64, c_void_p]),
     "qi_search_local_best": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
     "qi_search_set_best": (c_int, [c_void_p, POINTER(c_uint32), c_uint32]),
+    "qi_search_share_best": (c_int, [c_void_p, c_void_p]),
     "qi_search_reduce": (c_int, [c_void_p, POINTER(c_uint32), c_uint32, POINTER(Totals)]),
     "qi_search_witness": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32),
                                   POINTER(c_uint32)]),
@@ -166,7 +168,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.qi_abi_version() != 3:
+        if L.qi_abi_version() != 4:
             raise ImportError("libqi_amd.so ABI version mismatch")
         _lib = L
     return _lib

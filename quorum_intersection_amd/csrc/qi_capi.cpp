@@ -244,6 +244,7 @@ int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32
     res->devices = o.devices;
     res->units_moved = o.units_moved;
     res->t_device_init_ms = o.t_device_init_ms;
+    res->nodes_processed = o.processed_nodes;
     res->nodes = o.totals.nodes;
     res->evals += o.totals.evals;
     res->minq = o.totals.minq;
@@ -437,6 +438,14 @@ int qi_search_set_best(qi_search* s, const uint32_t* key, uint32_t depth) {
   std::vector<uint32_t> k(key, key + s->sd->key_words());
   s->sd->set_best(k, depth);
   return QI_OK;
+}
+
+int qi_search_share_best(qi_search* s, void* host_word) {
+  if (!s) return fail(QI_ERR_ARG, "null");
+  return guarded([&] {
+    s->sd->share_best((uint64_t*)host_word);
+    return QI_OK;
+  });
 }
 
 int qi_search_reduce(qi_search* s, const uint32_t* key, uint32_t depth, qi_totals* out) {

@@ -104,6 +104,15 @@ class SearchDevice {
   // Global best (preorder-first witness key) known to the caller, for pruning.
   virtual void set_best(const std::vector<uint32_t>& key, uint32_t depth) = 0;
   virtual bool best(Witness* w) const = 0;          // best witness found on this device
+  // Early termination across cooperating engines inside a chain (cpp:369-377 stops the
+  // whole search at the first disjoint pair): `host_word` is 8 bytes of host memory shared
+  // by the engines of one search (one process, or mapped into several); all ones = no
+  // witness.  After every launch the engine folds its best key into it (atomic minimum),
+  // and its kernels poll it like their own device-side key, so a witness found on one GPU
+  // prunes the others within a few launches instead of at the next host exchange.  The
+  // engine pins the word (hipHostRegister) if it is not HIP host memory already; null ends
+  // the sharing.  The caller resets the word between searches.
+  virtual void share_best(uint64_t* host_word) = 0;
   // Sums over every processed segment whose root precedes-or-equals `key` in preorder
   // (all segments when has_key == false).
   virtual Totals reduce(bool has_key, const std::vector<uint32_t>& key, uint32_t depth) = 0;
@@ -133,6 +142,10 @@ int device_cu_count(int device);
 void* device_alloc(int device, size_t bytes);
 void device_free(int device, void* p);
 void device_copy(void* dst, int dst_device, const void* src, int src_device, size_t bytes);
+// One 64-bit word of pinned host memory that every device can map (the engines' shared
+// best key, SearchDevice::share_best), initialised to all ones.
+uint64_t* pinned_word_alloc();
+void pinned_word_free(uint64_t* p);
 // Enable peer access from a to b (and b to a); false when the pair has no peer path
 // (copies then stage through the host inside the HIP runtime).
 bool enable_peer(int a, int b);

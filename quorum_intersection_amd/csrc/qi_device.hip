@@ -362,6 +362,17 @@ void device_copy(void* dst, int dst_device, const void* src, int src_device, siz
   HIP_CHECK(hipSetDevice(prev));
 }
 
+uint64_t* pinned_word_alloc() {
+  void* p = nullptr;
+  HIP_CHECK(hipHostMalloc(&p, 64, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
+  *(uint64_t*)p = ~0ull;
+  return (uint64_t*)p;
+}
+
+void pinned_word_free(uint64_t* p) {
+  if (p) (void)hipHostFree((void*)p);
+}
+
 bool enable_peer(int a, int b) {
   if (a == b) return true;
   int ab = 0, ba = 0;
@@ -763,6 +774,7 @@ class SearchDeviceImpl : public SearchDevice {
     (void)hipFree(red_);
     (void)hipFree(keydev_);
     (void)hipFree(wit_);
+    pinned_word_free(xbest_bridge_);
     for (auto* p : {sk_[0], sk_[1], sp_[0], sp_[1]}) (void)hipFree(p);
     (void)hipFree(stemp_);
     (void)hipEventDestroy(e0_);
@@ -836,6 +848,8 @@ class SearchDeviceImpl : public SearchDevice {
     HIP_CHECK(hipMemcpyAsync(ctr_, seed, sizeof seed, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(ctr_ + dev::CTR_WORDS, 0, (size_t)K * dev::CTR_WORDS * 4, stream_));
     std::memset((void*)hctr_, 0, (size_t)K * dev::HC_WORDS * 4);
+    for (uint32_t k = 0; k < K; ++k)  // no best key published yet
+      hctr_[(size_t)k * dev::HC_WORDS + dev::HC_BEST] = hctr_[(size_t)k * dev::HC_WORDS + dev::HC_BEST + 1] = 0xFFFFFFFFu;
 
     dev::SearchArgs a{};
     a.f = d_;
@@ -847,6 +861,7 @@ class SearchDeviceImpl : public SearchDevice {
     a.wit_cap = wit_cap_;
     a.totals = totals_;
     a.best64 = best64_;
+    a.xbest = xbest_dev_ ? xbest_dev_ : best64_;
     a.grow_budget = cfg_.grow_budget;
     a.run_budget = cfg_.run_budget;
     a.grace = cfg_.grace;
@@ -893,18 +908,28 @@ class SearchDeviceImpl : public SearchDevice {
       HIP_CHECK(hipEventRecord(ev_[k + 1], stream_));
     };
     auto hc = [&](uint32_t k) -> const volatile uint32_t* { return hctr_ + (size_t)k * dev::HC_WORDS; };
-    uint32_t enq = 0;
+    auto fold_best = [&](uint32_t k) {  // launch k's best key into the engines' shared word
+      if (!xbest_host_ || !hc(k)[dev::HC_DONE] || hc(k)[dev::HC_STOP]) return;
+      const uint64_t b = ((uint64_t)hc(k)[dev::HC_BEST + 1] << 32) | hc(k)[dev::HC_BEST];
+      uint64_t cur = __atomic_load_n(xbest_host_, __ATOMIC_RELAXED);
+      while (b < cur && !__atomic_compare_exchange_n(xbest_host_, &cur, b, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+      }
+      if (xbest_bridge_) __atomic_store_n(xbest_bridge_, std::min(cur, b), __ATOMIC_RELAXED);
+    };
+    uint32_t enq = 0, folded = 0;
     while (enq < K) {
       enqueue(enq++);
       if (enq > D) {  // wait for launch enq-1-D; stop enqueueing once the chain has run out
         const uint32_t j = enq - 1 - D;
         HIP_CHECK(hipEventSynchronize(ev_[j + 1]));
+        for (; folded <= j; ++folded) fold_best(folded);
         if (hc(j)[dev::HC_STOP] || hc(j)[dev::HC_OUT] == 0) break;
         if (until && hc(j)[dev::HC_OUT] >= until) break;
       }
     }
     HIP_CHECK(hipMemcpyAsync((void*)glob_host_, glob_, 8, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    for (; folded < enq; ++folded) fold_best(folded);
     const uint32_t g_wit = glob_host_[0], g_flags = glob_host_[1];
     if (g_flags & dev::FLAG_OUT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "search frontier buffer overflow");
     if (g_flags & dev::FLAG_WIT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "witness buffer overflow");
@@ -1086,6 +1111,28 @@ class SearchDeviceImpl : public SearchDevice {
     return true;
   }
 
+  void share_best(uint64_t* host_word) override {
+    DeviceGuard dg(device_);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    pinned_word_free(xbest_bridge_);
+    xbest_bridge_ = nullptr;
+    xbest_host_ = nullptr;
+    xbest_dev_ = nullptr;
+    if (!host_word) return;
+    if (((uintptr_t)host_word & 7u) != 0) throw Error(QI_ERR_ARG, "share_best: the word must be 8-byte aligned");
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, (void*)host_word, 0) != hipSuccess) {
+      // Not HIP host memory (a shared-memory page of several processes: the driver does not
+      // pin shared file mappings).  The kernels then poll a pinned word of this engine, and
+      // the host carries the minimum both ways after every launch (fold_best).
+      (void)hipGetLastError();
+      xbest_bridge_ = pinned_word_alloc();
+      HIP_CHECK(hipHostGetDevicePointer(&dp, (void*)xbest_bridge_, 0));
+    }
+    xbest_host_ = host_word;
+    xbest_dev_ = (const unsigned long long*)dp;
+  }
+
   Totals reduce(bool has_key, const std::vector<uint32_t>& key, uint32_t depth) override {
     // no witness: every segment counts, and the running totals are exactly those sums
     if (!has_key) return running_totals();
@@ -1146,6 +1193,7 @@ class SearchDeviceImpl : public SearchDevice {
     HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * dev::TOT_SHARDS * sizeof(unsigned long long), stream_));
     // no-witness best key; stream-ordered before every later launch, no host round trip
     HIP_CHECK(hipMemsetAsync(best64_, 0xFF, 8, stream_));
+    if (xbest_bridge_) __atomic_store_n(xbest_bridge_, ~0ull, __ATOMIC_RELAXED);  // a new search: no key yet
     has_best_ = false;
     has_local_best_ = false;
     sum_ms_ = 0;
@@ -1291,6 +1339,10 @@ class SearchDeviceImpl : public SearchDevice {
   uint64_t stops_ = 0;
   unsigned long long* totals_ = nullptr;
   unsigned long long* best64_ = nullptr;
+  uint64_t* xbest_host_ = nullptr;                  // the engines' shared best key (share_best)
+  const unsigned long long* xbest_dev_ = nullptr;   // its device view
+  uint64_t* xbest_bridge_ = nullptr;                // pinned copy the kernels poll when the shared
+                                                    // word itself is not HIP host memory
   unsigned long long* red_ = nullptr;
   uint32_t* keydev_ = nullptr;
   uint32_t* wit_ = nullptr;

@@ -129,6 +129,7 @@ SearchOutcome search_front_scc(const Graph& g, const std::vector<uint32_t>& scc,
   const bool found = sd->best(&w);
   o.totals = found ? sd->reduce(true, w.key, w.depth) : sd->running_totals();
   if (found) fill_witness(o, w, scc);
+  o.processed_nodes = found ? sd->running_totals().nodes : o.totals.nodes;
   o.launches = sd->launches();
   o.jit_launches = sd->specialized_launches();
   o.kernel_ms = sd->sum_kernel_ms();
@@ -168,6 +169,21 @@ SearchOutcome search_front_scc_sharded(const Graph& g, const std::vector<uint32_
   for (uint32_t e = 0; e < E; ++e) all.push_back(e);
   const uint64_t ub = eng[0]->unit_bytes();
   for (uint32_t e = 1; e < E; ++e) eng[e]->clear_frontier();  // the root lives on engine 0 only
+  // the engines' shared best key: a witness on one engine prunes the others inside their
+  // chains (the reference stops at the first disjoint pair, cpp:369-377)
+  struct PinnedWord {
+    uint64_t* p = pinned_word_alloc();
+    ~PinnedWord() { pinned_word_free(p); }
+  } shared_best;
+  struct Unshare {  // before the word is freed, whatever path leaves this function
+    std::vector<std::unique_ptr<SearchDevice>>& eng;
+    ~Unshare() {
+      for (auto& e : eng)
+        if (e) try { e->share_best(nullptr); } catch (...) {}
+    }
+  } unshare{eng};
+  if (E > 1 && !std::getenv("QI_NO_SHARED_BEST"))  // (diagnostics: exchange between chains only)
+    for (uint32_t e = 0; e < E; ++e) eng[e]->share_best(shared_best.p);
 
   // ---- (1) engine 0 grows the frontier from the root, (2) every engine keeps its deal ---
   const uint64_t target = sc.seed_units ? sc.seed_units : 2048ull * E;
@@ -254,6 +270,7 @@ SearchOutcome search_front_scc_sharded(const Graph& g, const std::vector<uint32_
     tot[e] = has_best ? eng[e]->reduce(true, best.key, best.depth) : eng[e]->running_totals();
   });
   for (uint32_t e = 0; e < E; ++e) {
+    o.processed_nodes += has_best ? eng[e]->running_totals().nodes : tot[e].nodes;
     o.totals.nodes += tot[e].nodes;
     o.totals.evals += tot[e].evals;
     o.totals.minq += tot[e].minq;

@@ -22,6 +22,8 @@ struct SearchOutcome {
   uint32_t engines = 1, devices = 1;
   uint64_t units_moved = 0;      // rebalancing hand-offs between engines
   uint64_t exchanges = 0;        // rounds of best-key / frontier-size exchange
+  uint64_t processed_nodes = 0;  // search nodes the engines ran, including those after the first
+                                 // witness in preorder (totals.nodes counts only the ones before)
   double t_device_init_ms = 0;   // peer access + engine device contexts (sharded runs)
 };
 

@@ -581,6 +581,10 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     if ((iter++ & 31u) == 0u) {
       const uint32_t h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       best64 = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      {  // the cooperating engines' shared best key (pinned host word; == best64 when alone)
+        const uint64_t xb = __hip_atomic_load(a.xbest, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        best64 = xb < best64 ? xb : best64;
+      }
       if (!dry && static_end + h >= n_in) {
         dry = true;
         if (!probing) limit = min(limit, steps + a.grace);
@@ -798,6 +802,9 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
         }
       }
       if (lane == 0) {
+        const unsigned long long bb = atomicMin(a.best64, ~0ull);  // this launch's best key, for the host
+        a.host_ctr[HC_BEST] = (uint32_t)bb;
+        a.host_ctr[HC_BEST + 1] = (uint32_t)(bb >> 32);
         cc[C_HALT] = left ? 1u : 0u;
         a.host_ctr[HC_HALT] = left ? 1u : 0u;
         out += left;

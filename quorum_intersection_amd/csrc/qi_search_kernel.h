@@ -267,7 +267,9 @@ enum : int {
                    // units left); the rest of the chain does nothing and the host sorts
                    // the frontier into preorder before it goes on
   CTR_WORDS = 64,
-  HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6, HC_WORDS = 8
+  HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6,
+  HC_BEST = 8,     // u64 (two words): the device-side best key after this launch
+  HC_WORDS = 16
 };
 // Output capacity per launch: n_in (carried-over units) + per used lane SPILL_RESERVE(S)
 // units for its one final spill (current node, top of stack, S stacked entries, a claimed
@@ -295,6 +297,10 @@ struct SearchArgs {
   unsigned long long* totals;    // [TOT_SHARDS][16]: nodes, evals, minq, zero_fallback, rounds, units, ...
   unsigned long long* best64;    // device-side best witness, best_pack(): exact when MW == 1,
                                  // the first 64 path bits (conservative pruning) otherwise
+  const unsigned long long* xbest;  // the same key over every cooperating engine (other streams,
+                                 // GPUs or processes): a word in pinned host memory that the
+                                 // hosts fold their launches' best keys into and every kernel
+                                 // polls; == best64 for a lone engine
   uint32_t grow_budget;          // per-lane node budget while the frontier is below half the lanes
   uint32_t run_budget;
   uint32_t grace;                // extra steps per lane once the unit queue is dry
@@ -463,6 +469,12 @@ constexpr int stamp_bucket(int f) {
 #ifndef QI_POLL_EVERY
 #define QI_POLL_EVERY 384
 #endif
+// The best key (this engine's and the cooperating engines' shared one) is polled more often:
+// every QI_POLL_EVERY / QI_BEST_POLLS iterations (a witness found elsewhere prunes sooner);
+// the queue head is looked at in every QI_BEST_POLLS-th of these polls.
+#ifndef QI_BEST_POLLS
+#define QI_BEST_POLLS 6
+#endif
 // Fast steps: up to QI_FAST_STEPS lean iterations run between two full ones while at least
 // QI_FAST_MIN lanes can pop or process a node without any service (no unit to install, no
 // quorum leaf, no full stack) and no witness is known (nothing to prune).  The full
@@ -584,6 +596,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint32_t iter = 0;        // wave-uniform: iterations so far, fast steps included
   uint32_t next_poll = 0;   // the poll is due in the first full iteration with iter >= next_poll
   bool poll_issued = true;  // its loads are in flight (the first ones are issued before the loop)
+  uint32_t poll_n = 0;      // polls so far (the queue head counts in every QI_BEST_POLLS-th)
   // the next unit of this lane: claimed index (= its log record index) + (PREFETCH) its
   // words in registers; installed at the start of the iteration after the lane ran out
   bool fpend = false;
@@ -610,9 +623,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // their latency hides behind that iteration (the first poll, at iteration 0, reads these)
   uint32_t poll_h = 0;
   uint64_t poll_b = ~0ull;
+  auto poll_best = [&]() -> uint64_t {  // lane 0: this engine's best and the shared one
+    const uint64_t b0 = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b1 = __hip_atomic_load(a.xbest, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return b0 < b1 ? b0 : b1;
+  };
   if (lane == 0) {
     poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    poll_b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    poll_b = poll_best();
   }
 
   auto load_unit = [&]() {  // issue the loads of unit fidx (consumed at install)
@@ -1013,7 +1031,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // subtrees while the rest idle.
     if (poll_issued && iter >= next_poll) {
       poll_issued = false;
-      next_poll = iter + (uint32_t)QI_POLL_EVERY;
+      next_poll = iter + (uint32_t)(QI_POLL_EVERY / QI_BEST_POLLS);
       uint32_t h = 0;
       uint64_t b = ~0ull;
       if (lane == 0) {
@@ -1022,7 +1040,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
       h = lane0(h);
       best64 = lane0(b);
-      if (!dry && h >= n_in) {
+      const bool head_poll = (poll_n++ % (uint32_t)QI_BEST_POLLS) == 0u;
+      if (head_poll && !dry && h >= n_in) {
         dry = true;
         limit = min(limit, steps + a.grace);
       }
@@ -1031,7 +1050,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       poll_issued = true;
       if (lane == 0) {
         poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        poll_b = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        poll_b = poll_best();
       }
     }
     ++iter;
@@ -1413,6 +1432,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (lane == 0) {
         hd = atomicAdd(&cc[C_HEAD], 0u);
         out = atomicAdd(&cc[C_OUT], 0u);
+        // this launch's best key for the host (folded into the engines' shared word)
+        const unsigned long long bb = atomicMin(a.best64, ~0ull);
+        a.host_ctr[HC_BEST] = (uint32_t)bb;
+        a.host_ctr[HC_BEST + 1] = (uint32_t)(bb >> 32);
       }
       hd = lane0(hd);
       out = lane0(out);

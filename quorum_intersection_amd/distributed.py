@@ -26,6 +26,8 @@ gloo process group.
 from __future__ import annotations
 
 import ctypes
+import mmap
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -161,6 +163,12 @@ class DeviceSearch(SearchBackend):
         k = (ctypes.c_uint32 * self.key_words)(*key[0])
         self._c.check(self.L.qi_search_set_best(self.h, k, key[1]))
 
+    def share_best(self, shared: Optional["SharedBest"]):
+        """Fold this engine's best key into `shared` after every launch and let its kernels
+        poll it (qi_search_share_best); None ends the sharing."""
+        self._c.check(self.L.qi_search_share_best(self.h, ctypes.c_void_p(shared.address if shared else None)))
+        self._shared = shared  # keeps the mapping alive while the engine uses it
+
     def reduce(self, key):
         t = self._c.Totals()
         if key is None:
@@ -187,6 +195,66 @@ class DeviceSearch(SearchBackend):
         l1, l2 = ctypes.c_uint32(), ctypes.c_uint32()
         self._c.check(self.L.qi_search_witness(self.h, q1, ctypes.byref(l1), q2, ctypes.byref(l2)))
         return list(q1)[: l1.value], list(q2)[: l2.value]
+
+
+class SharedBest:
+    """The ranks' shared best-witness key: one 64-bit word in a POSIX shared-memory page that
+    every rank of the node maps (the search runs on the GPUs of ONE node).  Each rank's
+    engine folds its launches' best keys into it and its kernels poll it, so a witness found
+    on one GPU prunes the others inside their chains of launches; the exact result still
+    comes from the all_gather of keys and the preorder-filtered reduction."""
+
+    def __init__(self, name: str, create: bool):
+        self.path = os.path.join("/dev/shm", name)
+        flags = os.O_RDWR | (os.O_CREAT if create else 0)
+        fd = os.open(self.path, flags, 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, mmap.PAGESIZE)
+            self.mm = mmap.mmap(fd, mmap.PAGESIZE)
+        finally:
+            os.close(fd)
+        self.created = create
+        self._word = ctypes.c_uint64.from_buffer(self.mm)
+        self.address = ctypes.addressof(self._word)
+        if create:
+            self.reset()
+
+    def reset(self) -> None:
+        self._word.value = 0xFFFFFFFFFFFFFFFF
+
+    @property
+    def value(self) -> int:
+        return int(self._word.value)
+
+    def close(self) -> None:
+        if getattr(self, "mm", None) is not None:
+            del self._word
+            try:
+                self.mm.close()
+            except BufferError:
+                pass
+            self.mm = None
+            if self.created:
+                try:
+                    os.unlink(self.path)
+                except OSError:
+                    pass
+
+    @staticmethod
+    def for_group(group=None, tag: str = "") -> "SharedBest":
+        """Collective: group rank 0 creates the page, the others map it."""
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        name = [f"qi_best_{os.getpid()}_{tag}_{time.time_ns()}" if rank == 0 else None]
+        sb = SharedBest(name[0], True) if rank == 0 else None
+        if dist.is_initialized() and dist.get_world_size(group) > 1:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(name, src=src, group=group)
+        if sb is None:
+            sb = SharedBest(name[0], False)
+        if dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.barrier(group=group)  # every rank has mapped it before rank 0 may unlink
+        return sb
 
 
 # ------------------------------------------------------------------------------------
@@ -294,13 +362,19 @@ def _settle(t: torch.Tensor) -> None:
 
 
 def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int = 1 << 17,
-                       rebalance: bool = True, min_move: int = 64, seed_units: int = 0) -> DistResult:
-    """Run one full search across the ranks of `group`; every rank returns the result."""
+                       rebalance: bool = True, min_move: int = 64, seed_units: int = 0,
+                       shared: Optional[SharedBest] = None) -> DistResult:
+    """Run one full search across the ranks of `group`; every rank returns the result.
+    shared: the ranks' SharedBest page (already given to every rank's engine with
+    share_best): rank 0 resets it here, before the frontier broadcast that starts the
+    other ranks."""
     if dist.is_available() and dist.is_initialized():
         rank, world = dist.get_rank(group), dist.get_world_size(group)
     else:
         rank, world = 0, 1
     t0 = time.perf_counter()
+    if shared is not None and rank == 0:
+        shared.reset()
     be.restart()
     launches = 0
     moved = 0

@@ -37,20 +37,25 @@ def main():
     import torch
     import torch.distributed as dist
     import quorum_intersection_amd as qa
-    from quorum_intersection_amd.distributed import DeviceSearch, distributed_search
+    from quorum_intersection_amd.distributed import DeviceSearch, SharedBest, distributed_search
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     fb = qa.FBAS(workload_text(name), device=0)
     be = DeviceSearch(fb, jit=2, batch=batch)
+    shared = SharedBest.for_group(tag=port)  # the ranks' shared best key, as bench.py --gpus N sets it up
+    be.share_best(shared)
     print(f"rank {rank}: engine ready, {name}", flush=True)
-    r = distributed_search(be, device=torch.device("cpu"), seed_units=seed_units)
+    r = distributed_search(be, device=torch.device("cpu"), seed_units=seed_units, shared=shared)
+    print(f"rank {rank}: shared best word {shared.value:#x}", flush=True)
+    be.share_best(None)
     print(f"rank {rank}: nodes {r.nodes} moved {r.moved_units}", flush=True)
     if rank == 0:
         with open(out, "w") as fh:
             json.dump({"verdict": r.verdict, "nodes": r.nodes, "evals": r.evals, "minq": r.minq, "q1": r.q1, "q2": r.q2,
                        "launches": r.launches, "moved_units": r.moved_units, "world": world}, fh)
     dist.barrier()
+    shared.close()
     dist.destroy_process_group()
 
 

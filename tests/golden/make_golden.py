@@ -47,6 +47,8 @@ def big_instances():
     # FBAS without the pair (plant=False), whose full search sizes the tree
     yield "planted_deep_8_512", fbas_gen.planted_deep(8, 512)
     yield "planted_deep_8_512_intact", fbas_gen.planted_deep(8, 512, plant=False)
+    # a 35-vertex tier (two-word masks): the first witness 14.96 M nodes into the tree (~100 s)
+    yield "planted_deep_9_512", fbas_gen.planted_deep(9, 512)
 
 
 def big(only):

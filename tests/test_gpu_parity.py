@@ -562,6 +562,42 @@ def test_sharded_planted_deep_exact(engines):
     g = BIG["planted_deep_8_512"]
     d = qa.FBAS(fbas_gen.planted_deep(8, 512)).solve_stats(engines=engines, device_mask=1, jit=2)
     _cmp(d, g, "planted_deep_8_512")
+    assert d["nodes_processed"] >= d["nodes"]
+
+
+def test_shared_best_key_prunes_other_engines(monkeypatch):
+    # cpp:369-377 stops at the first disjoint pair.  Across engines the best key travels in a
+    # shared pinned word that every kernel polls: a witness found by one engine prunes the
+    # others inside their chains.  With the word switched off the engines only learn of it
+    # between chains.  Counts and witness are exact either way; the work after the witness
+    # (nodes_processed - nodes) must not grow with sharing on.
+    # planted_deep(9, 512): a 35-vertex tier (two-word masks), the first witness 14.96 M nodes
+    # into the tree, so every engine's share spans several chains' worth of launches.
+    g = BIG["planted_deep_9_512"]
+    text = fbas_gen.planted_deep(9, 512)
+    runs = {}
+    for mode in ("shared", "unshared"):
+        if mode == "unshared":
+            monkeypatch.setenv("QI_NO_SHARED_BEST", "1")
+        best = None
+        for _ in range(2):
+            d = qa.FBAS(text).solve_stats(engines=8, device_mask=1, jit=2)
+            _cmp(d, g, f"planted_deep_9_512 {mode}")
+            waste = d["nodes_processed"] - d["nodes"]
+            best = waste if best is None else min(best, waste)
+        runs[mode] = best
+    print("post-witness nodes:", runs)
+    assert runs["shared"] <= 1.02 * runs["unshared"], runs
+
+
+def test_planted_deep_two_word_exact():
+    # the same 35-vertex early-exit instance on one engine, both kernels
+    g = BIG["planted_deep_9_512"]
+    text = fbas_gen.planted_deep(9, 512)
+    for jit in (2, 1):
+        d = qa.FBAS(text).solve_stats(jit=jit)
+        _cmp(d, g, "planted_deep_9_512")
+    _validate_witness(text, d["q1"], d["q2"], g["front"])
 
 
 # ---- one process per rank over the real engine (the code path of bench.py --gpus N) --------
@@ -591,6 +627,8 @@ def test_distributed_search_real_engine_two_ranks(name, batch, seed_units, tmp_p
             if p.poll() is None:
                 p.kill()
     assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+    if name.startswith("planted_deep"):  # the witness key reached the ranks' shared word
+        assert all("shared best word" in lg and "shared best word 0xffffffffffffffff" not in lg for lg in logs), logs
     d = json.load(open(out))
     g = BIG[name] if name in BIG else GOLD[name]
     assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (g["verdict"], g["nodes"], g["evals"] - g["scc_evals"],

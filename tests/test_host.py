@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(L, n), n
         assert n in _capi.SIGNATURES, f"{n} missing from the ctypes signature table"
-    assert L.qi_abi_version() == 3
+    assert L.qi_abi_version() == 4
 
 
 def test_library_has_gfx950_code_object():
