@@ -38,7 +38,9 @@ std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g);
 // ----------------------------------------------------------------------------------
 struct SearchConfig {
   uint32_t max_blocks = 0;       // 0 = CUs * 8
-  uint32_t grow_budget = 2;      // per-lane node budget while the frontier is small (sweeps: 2 < 4 < 8 < 16 < 48 ms)
+  uint32_t grow_budget = 3;      // per-lane node budget while the frontier is small (2 / 3 / 4 / 6: 2.25 /
+                                 // 2.19 / 3.28 / 3.46 ms on the bench workload, 0.47 / 0.41 / 0.43 / 0.45 ms
+                                 // on two_tier(8, 192))
   uint32_t run_budget = 4096;    // per-lane node budget once the frontier fills the GPU
   uint32_t grace = 16;           // per-lane steps after the unit queue runs dry (8/12/16/20/24: 2.27/2.26/2.22/2.32/2.39 ms)
   uint32_t evict_max = 32;       // per-lane stack evictions per launch (bounds the output; 8 stalls deep

@@ -75,9 +75,10 @@ __global__ __launch_bounds__(64) void ordered_kernel(OrdArgs oa) {
   ordered_body<MW, TW>(oa);
 }
 
-// Fold a host-known best witness into the device-side one (1-word keys).
-static __global__ void min_best_kernel(unsigned long long* best64, unsigned long long v) {
+// Fold a host-known best witness into the device-side one and its polled replicas (1-word keys).
+static __global__ void min_best_kernel(unsigned long long* best64, uint32_t* poll_rep, unsigned long long v) {
   if (threadIdx.x == 0) atomicMin(best64, v);
+  if (threadIdx.x < POLL_REPS) atomicMin((unsigned long long*)(poll_rep + (size_t)threadIdx.x * 32), v);
 }
 
 // A rank's share of a broadcast frontier, dealt in rounds of `stride` units with a rotating
@@ -615,6 +616,7 @@ class SearchDeviceImpl : public SearchDevice {
     };
     // tuning overrides for experiments (profiling only; defaults are the measured best)
     if (const char* e = std::getenv("QI_GRACE")) cfg_.grace = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_GROW")) cfg_.grow_budget = (uint32_t)std::max(1, std::atoi(e));
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
@@ -706,6 +708,8 @@ class SearchDeviceImpl : public SearchDevice {
     lap("chain events");
     totals_ = dalloc<unsigned long long>(16 * dev::TOT_SHARDS);
     best64_ = dalloc<unsigned long long>(1);
+    poll_rep_ = dalloc<uint32_t>((size_t)dev::POLL_REPS * 32);
+    HIP_CHECK(hipMemsetAsync(poll_rep_, 0xFF, (size_t)dev::POLL_REPS * 128, stream_));
     red_ = dalloc<unsigned long long>(4);
     keydev_ = dalloc<uint32_t>(dev::KEY_WORDS_MAX);
     wit_cap_ = 1u << 16;
@@ -771,6 +775,7 @@ class SearchDeviceImpl : public SearchDevice {
     for (auto& e : ev_) (void)hipEventDestroy(e);
     (void)hipFree(totals_);
     (void)hipFree(best64_);
+    (void)hipFree(poll_rep_);
     (void)hipFree(red_);
     (void)hipFree(keydev_);
     (void)hipFree(wit_);
@@ -862,6 +867,7 @@ class SearchDeviceImpl : public SearchDevice {
     a.totals = totals_;
     a.best64 = best64_;
     a.xbest = xbest_dev_ ? xbest_dev_ : best64_;
+    a.poll_rep = poll_rep_;
     a.grow_budget = cfg_.grow_budget;
     a.run_budget = cfg_.run_budget;
     a.grace = cfg_.grace;
@@ -882,7 +888,7 @@ class SearchDeviceImpl : public SearchDevice {
     static_assert(MW <= dev::KEY_WORDS_MAX, "path key wider than the key buffers");
     for (int w = 0; w < dev::KEY_WORDS_MAX; ++w) a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
     if (MW == 1 && has_best_ && best_dirty_) {  // 1-word keys: the device best is exact; fold the host's in
-      hipLaunchKernelGGL(dev::min_best_kernel, dim3(1), dim3(64), 0, stream_, best64_,
+      hipLaunchKernelGGL(dev::min_best_kernel, dim3(1), dim3(64), 0, stream_, best64_, poll_rep_,
                          ((unsigned long long)best_key_[0] << 32) | best_depth_);
       HIP_CHECK(hipGetLastError());
     }
@@ -894,6 +900,8 @@ class SearchDeviceImpl : public SearchDevice {
       a.prev = ctr_ + (size_t)k * dev::CTR_WORDS;
       a.counters = ctr_ + (size_t)(k + 1) * dev::CTR_WORDS;
       a.host_ctr = hctr_dev_ + (size_t)k * dev::HC_WORDS;
+      if (++seq_ == 0xFFFFFFFFu) seq_ = 1;  // (the replicas' reset value is never a sequence number)
+      a.seq = seq_;
       if constexpr (ORD) {
         dev::OrdArgs oa = ord_;
         oa.a = a;
@@ -1193,6 +1201,7 @@ class SearchDeviceImpl : public SearchDevice {
     HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * dev::TOT_SHARDS * sizeof(unsigned long long), stream_));
     // no-witness best key; stream-ordered before every later launch, no host round trip
     HIP_CHECK(hipMemsetAsync(best64_, 0xFF, 8, stream_));
+    HIP_CHECK(hipMemsetAsync(poll_rep_, 0xFF, (size_t)dev::POLL_REPS * 128, stream_));
     if (xbest_bridge_) __atomic_store_n(xbest_bridge_, ~0ull, __ATOMIC_RELAXED);  // a new search: no key yet
     has_best_ = false;
     has_local_best_ = false;
@@ -1339,6 +1348,8 @@ class SearchDeviceImpl : public SearchDevice {
   uint64_t stops_ = 0;
   unsigned long long* totals_ = nullptr;
   unsigned long long* best64_ = nullptr;
+  uint32_t* poll_rep_ = nullptr;                    // [POLL_REPS][32]: polled best key + dry flag lines
+  uint32_t seq_ = 0;                                // launch sequence numbers
   uint64_t* xbest_host_ = nullptr;                  // the engines' shared best key (share_best)
   const unsigned long long* xbest_dev_ = nullptr;   // its device view
   uint64_t* xbest_bridge_ = nullptr;                // pinned copy the kernels poll when the shared

@@ -383,7 +383,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
   // a lone root unit first goes depth-first on one lane: an early witness (cpp:369-377)
   // then ends the search before the parallel growth expands the subtrees after it
   const bool probing = n_in == 1u && oa.probe;  // (no grace: nothing else is left to claim)
-  const uint32_t budget = probing ? oa.probe : launch_budget(a, n_in);
+  const uint32_t budget = probing ? oa.probe : launch_budget(a, n_in, false);
   uint32_t* const st = oa.ostack + (size_t)blockIdx.x * (oa.smax * SEW * WAVE);
 #define OST(lvl, w) st[((size_t)(lvl) * SEW + (w)) * WAVE + lane]
 
@@ -581,9 +581,11 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
     if ((iter++ & 31u) == 0u) {
       const uint32_t h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       best64 = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      {  // the cooperating engines' shared best key (pinned host word; == best64 when alone)
+      if (blockIdx.x == 0 && lane == 0 && a.xbest != a.best64) {
+        // block 0 forwards the cooperating engines' shared key (pinned host word) into this
+        // device's word, where every wave polls it
         const uint64_t xb = __hip_atomic_load(a.xbest, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        best64 = xb < best64 ? xb : best64;
+        if (xb < best64) atomicMin(a.best64, (unsigned long long)xb);
       }
       if (!dry && static_end + h >= n_in) {
         dry = true;

@@ -266,6 +266,8 @@ enum : int {
   C_HALT = 37,     // 1: this launch carried units over (its lanes ran out of budget with
                    // units left); the rest of the chain does nothing and the host sorts
                    // the frontier into preorder before it goes on
+  C_PEAKED = 38,   // 1: this or an earlier launch of the chain ran with the run budget: the
+                   // frontier has covered the lanes once, what follows is its decay
   CTR_WORDS = 64,
   HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6,
   HC_BEST = 8,     // u64 (two words): the device-side best key after this launch
@@ -280,6 +282,7 @@ enum : int {
 __host__ __device__ constexpr uint32_t spill_reserve(uint32_t smax) { return smax + 4u; }
 constexpr int TOT_SHARDS = 64;  // running totals: [TOT_SHARDS][16] u64, shard = block % 64
 
+constexpr int POLL_REPS = 64;
 constexpr int KEY_WORDS_MAX = 32;  // path-key words of the largest kernel shape (MW <= 32)
 struct SearchArgs {
   LocalDev f;
@@ -299,8 +302,14 @@ struct SearchArgs {
                                  // the first 64 path bits (conservative pruning) otherwise
   const unsigned long long* xbest;  // the same key over every cooperating engine (other streams,
                                  // GPUs or processes): a word in pinned host memory that the
-                                 // hosts fold their launches' best keys into and every kernel
-                                 // polls; == best64 for a lone engine
+                                 // hosts fold their launches' best keys into; block 0 of a launch
+                                 // polls it and forwards it; == best64 for a lone engine
+  uint32_t* poll_rep;            // [POLL_REPS][32 words] what the waves poll, replicated on 128-B
+                                 // lines (wave b reads line b % POLL_REPS): words 0-1 the best key,
+                                 // word 2 the sequence number of the last launch seen dry.  Every
+                                 // wave polling ONE best key / queue head serialised at that line
+                                 // (~25 ns per access: 0.8 ms per search at 64-iteration polls).
+  uint32_t seq;                  // this launch's sequence number (unique per engine, never 0xFFFFFFFF)
   uint32_t grow_budget;          // per-lane node budget while the frontier is below half the lanes
   uint32_t run_budget;
   uint32_t grace;                // extra steps per lane once the unit queue is dry
@@ -355,10 +364,13 @@ __device__ __forceinline__ void key_prefix_bit(uint32_t (&K)[MW], uint32_t de) {
 // Per-lane node budget of a launch from how well its input covers the resident lanes:
 // a small frontier grows (a few nodes per lane, then spill: more units next launch); a
 // frontier that covers most lanes runs long.
-__device__ __forceinline__ uint32_t launch_budget(const SearchArgs& a, uint32_t n_in) {
+// Once a launch of the chain has run with the run budget (`peaked`), the rest do too: a
+// shrinking frontier holds deep, small subtrees, and relaunching them every grow-budget
+// steps only adds launches (their lanes stop `grace` steps after the queue runs dry anyway).
+__device__ __forceinline__ uint32_t launch_budget(const SearchArgs& a, uint32_t n_in, bool peaked) {
   const uint64_t lanes8 = (uint64_t)gridDim.x * WAVE;
   const uint64_t n8 = (uint64_t)n_in * 8u;
-  return n8 < lanes8 * a.run_at ? a.grow_budget : a.run_budget;
+  return (!peaked && n8 < lanes8 * a.run_at) ? a.grow_budget : a.run_budget;
 }
 
 // Wave-aggregated reservation of n (per lane, n < 2^NB) slots on a global counter: the
@@ -469,9 +481,9 @@ constexpr int stamp_bucket(int f) {
 #ifndef QI_POLL_EVERY
 #define QI_POLL_EVERY 384
 #endif
-// The best key (this engine's and the cooperating engines' shared one) is polled more often:
-// every QI_POLL_EVERY / QI_BEST_POLLS iterations (a witness found elsewhere prunes sooner);
-// the queue head is looked at in every QI_BEST_POLLS-th of these polls.
+// The best key is polled more often than the dry flag acts: every QI_POLL_EVERY /
+// QI_BEST_POLLS iterations (a witness found elsewhere prunes sooner); the dry flag counts in
+// every QI_BEST_POLLS-th of these polls.
 #ifndef QI_BEST_POLLS
 #define QI_BEST_POLLS 6
 #endif
@@ -485,6 +497,12 @@ constexpr int stamp_bucket(int f) {
 #endif
 #ifndef QI_FAST_MIN
 #define QI_FAST_MIN 56
+#endif
+// run budget for every launch after the first one that had it (see launch_budget): 0 off,
+// 1 always, 2 only while no witness is known (measured: two_tier(8,192) 0.43 / 0.40 / 0.41 ms,
+// planted_deep 0.97 / 1.15 / 0.97 ms, the bench workload 2.21 / 2.18 / 2.21 ms)
+#ifndef QI_DECAY_RUN
+#define QI_DECAY_RUN 2
 #endif
 // claim the next units (and flush records) right after the installs instead of after the push
 #ifndef QI_CLAIM_FIRST
@@ -540,7 +558,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // evictions share what the final spills and the carried-over units leave of out_cap
   const uint64_t spill_need = (uint64_t)n_in + (uint64_t)nb_used * WAVE * spill_reserve(SMAX);
   const uint32_t evict_pool = spill_need < (uint64_t)a.out_cap ? (uint32_t)((uint64_t)a.out_cap - spill_need) : 0u;
-  const uint32_t budget = launch_budget(a, n_in);
+  // (QI_DECAY_RUN 2: not once a witness is known -- short launches then prune sooner)
+  const bool peaked_in = QI_DECAY_RUN && pc[C_PEAKED] != 0u && (QI_DECAY_RUN == 1 || *a.best64 == ~0ull);
+  const uint32_t budget = launch_budget(a, n_in, peaked_in);
   {
     // the final spills, and at least evict_max evictions per used lane
     const uint64_t need_out = spill_need + (uint64_t)nb_used * WAVE * (uint64_t)a.evict_max;
@@ -551,6 +571,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       cc[C_LOGB] = log_base;
       cc[C_STATIC] = static_end;
       cc[C_STOP] = stop ? 1u : 0u;
+      cc[C_PEAKED] = (peaked_in || (!stop && nb_used != 0 && budget == a.run_budget)) ? 1u : 0u;
       if (stop || nb_used == 0) {  // nothing runs: publish now (else the last block does)
         cc[C_LOGN] = log_base;
         a.host_ctr[HC_LOGN] = log_base;
@@ -621,17 +642,22 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint64_t best64 = ~0ull;
   // lane 0's poll loads are issued one iteration before the poll that reads them, so
   // their latency hides behind that iteration (the first poll, at iteration 0, reads these)
-  uint32_t poll_h = 0;
-  uint64_t poll_b = ~0ull;
-  auto poll_best = [&]() -> uint64_t {  // lane 0: this engine's best and the shared one
-    const uint64_t b0 = __hip_atomic_load(a.best64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t b1 = __hip_atomic_load(a.xbest, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return b0 < b1 ? b0 : b1;
+  uint32_t* const my_rep = a.poll_rep + (size_t)(blockIdx.x & (POLL_REPS - 1)) * 32;
+  uint32_t poll_d = 0;      // lane 0: the polled dry-launch sequence number
+  uint64_t poll_b = ~0ull;  // lane 0: the polled best key
+  uint64_t poll_x = ~0ull;  // lane 0 of block 0: the cooperating engines' shared key
+  const bool forwarder = blockIdx.x == 0 && a.xbest != a.best64;  // wave-uniform
+  auto issue_poll = [&]() {  // lane 0
+    poll_b = __hip_atomic_load((unsigned long long*)my_rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    poll_d = __hip_atomic_load(my_rep + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (forwarder) poll_x = __hip_atomic_load(a.xbest, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   };
-  if (lane == 0) {
-    poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    poll_b = poll_best();
-  }
+  // a best key into the canonical word and every polled replica (witnesses are rare)
+  auto publish_best = [&](unsigned long long key) {
+    atomicMin(a.best64, key);
+    for (int r = 0; r < POLL_REPS; ++r) atomicMin((unsigned long long*)(a.poll_rep + (size_t)r * 32), key);
+  };
+  if (lane == 0) issue_poll();
 
   auto load_unit = [&]() {  // issue the loads of unit fidx (consumed at install)
     if constexpr (PREFETCH) {
@@ -781,7 +807,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       } else {
         atomicOr(&a.glob[1], FLAG_WIT_OVERFLOW);
       }
-      atomicMin(a.best64, (unsigned long long)best_pack<MW>(K, depth));
+      publish_best((unsigned long long)best_pack<MW>(K, depth));
       nst = 0;  // everything left in this unit follows the witness in preorder
       tvalid = false;
     }
@@ -803,6 +829,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         base = lane0(base);
         if (base >= n_in) {
           pool_dead = true;
+          // tell the waves that poll this line: no unit is left to claim in this launch
+          if (lane == 0) __hip_atomic_store(my_rep + 2, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
         pool_next = base;
@@ -1024,34 +1052,35 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // past the budget is spilled below)
     if (!has && !tvalid && nst == 0 && !fpend && (steps >= limit || pool_dead)) done = true;
 
-    // Every QI_POLL_EVERY iterations poll the global head and the device-side best key
-    // (loads issued one full iteration ahead).  Once no unit is left to claim anywhere, every
-    // lane gets a short grace period and then spills: the next launch spreads the
-    // remaining subtrees over all lanes instead of letting a few lanes grind through deep
-    // subtrees while the rest idle.
+    // Poll this wave's line (loads issued one full iteration ahead): the best key, and
+    // whether a wave sharing the line found the unit queue dry.  Once no unit is left to
+    // claim, every lane gets a short grace period and then spills: the next launch spreads
+    // the remaining subtrees over all lanes instead of letting a few lanes grind through
+    // deep subtrees while the rest idle.
     if (poll_issued && iter >= next_poll) {
       poll_issued = false;
       next_poll = iter + (uint32_t)(QI_POLL_EVERY / QI_BEST_POLLS);
-      uint32_t h = 0;
+      uint32_t d = 0;
       uint64_t b = ~0ull;
       if (lane == 0) {
-        h = static_end + poll_h;
+        d = poll_d;
         b = poll_b;
+        if (forwarder && poll_x < b) {  // a key from another engine: into this device's words
+          b = poll_x;
+          publish_best(poll_x);
+        }
       }
-      h = lane0(h);
+      d = lane0(d);
       best64 = lane0(b);
-      const bool head_poll = (poll_n++ % (uint32_t)QI_BEST_POLLS) == 0u;
-      if (head_poll && !dry && h >= n_in) {
+      const bool dry_poll = (poll_n++ % (uint32_t)QI_BEST_POLLS) == 0u;
+      if (dry_poll && !dry && d == a.seq) {
         dry = true;
         limit = min(limit, steps + a.grace);
       }
     } else if (!poll_issued && iter + 2u * ((uint32_t)QI_FAST_STEPS + 1u) >= next_poll) {
       // at least one full iteration before the poll that reads them
       poll_issued = true;
-      if (lane == 0) {
-        poll_h = __hip_atomic_load(&cc[C_HEAD], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        poll_b = poll_best();
-      }
+      if (lane == 0) issue_poll();
     }
     ++iter;
 
