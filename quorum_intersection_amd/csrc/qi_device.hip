@@ -913,7 +913,27 @@ class SearchDeviceImpl : public SearchDevice {
         hipLaunchKernelGGL((dev::search_kernel<MW, TW, SMAX>), dim3(blocks), dim3(64), shm_, stream_, a);
       }
       HIP_CHECK(hipGetLastError());
-      HIP_CHECK(hipEventRecord(ev_[k + 1], stream_));
+      if (trace_) HIP_CHECK(hipEventRecord(ev_[k + 1], stream_));  // per-launch times: diagnostics only
+    };
+    // Launch k's published flag word in pinned host memory: the host spins on it instead of
+    // recording and waiting for an event per launch (an event between two chained launches
+    // cost ~10 us of the ~13 us per launch boundary).
+    auto wait_flag = [&](uint32_t k) -> uint64_t {
+      volatile uint64_t* fp = (volatile uint64_t*)(hctr_ + (size_t)k * dev::HC_WORDS + dev::HC_FLAG);
+      for (uint32_t spin = 0;; ++spin) {
+        const uint64_t v = __atomic_load_n((const uint64_t*)fp, __ATOMIC_ACQUIRE);
+        if (v >> 63) return v;
+        if ((spin & 0xFFFu) == 0xFFFu) {  // a fault or a drained stream must not spin for ever
+          const hipError_t q = hipStreamQuery(stream_);
+          if (q == hipSuccess) {
+            const uint64_t v2 = __atomic_load_n((const uint64_t*)fp, __ATOMIC_ACQUIRE);
+            if (v2 >> 63) return v2;
+            throw Error(QI_ERR_DEVICE, "search launch did not publish its counters");
+          }
+          if (q != hipErrorNotReady) throw Error(QI_ERR_DEVICE, std::string("search chain: ") + hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+      }
     };
     auto hc = [&](uint32_t k) -> const volatile uint32_t* { return hctr_ + (size_t)k * dev::HC_WORDS; };
     auto fold_best = [&](uint32_t k) {  // launch k's best key into the engines' shared word
@@ -929,12 +949,13 @@ class SearchDeviceImpl : public SearchDevice {
       enqueue(enq++);
       if (enq > D) {  // wait for launch enq-1-D; stop enqueueing once the chain has run out
         const uint32_t j = enq - 1 - D;
-        HIP_CHECK(hipEventSynchronize(ev_[j + 1]));
+        const uint64_t fl = wait_flag(j);
         for (; folded <= j; ++folded) fold_best(folded);
-        if (hc(j)[dev::HC_STOP] || hc(j)[dev::HC_OUT] == 0) break;
-        if (until && hc(j)[dev::HC_OUT] >= until) break;
+        if (((fl >> 62) & 1u) || (uint32_t)fl == 0u) break;
+        if (until && (uint32_t)fl >= until) break;
       }
     }
+    if (!trace_) HIP_CHECK(hipEventRecord(ev_[1], stream_));  // the whole chain, first launch to last
     HIP_CHECK(hipMemcpyAsync((void*)glob_host_, glob_, 8, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
     for (; folded < enq; ++folded) fold_best(folded);
@@ -951,10 +972,16 @@ class SearchDeviceImpl : public SearchDevice {
     uint64_t n_next = n_, log_next = lc.used;
     bool halted = false;
     int cur_next = cur_;
-    for (uint32_t j = 0; j < enq; ++j) {
+    if (trace_) {
+      for (uint32_t j = 0; j < enq; ++j) {
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, ev_[j], ev_[j + 1]));
+        si.dispatch_ms += ms;
+      }
+    } else {
       float ms = 0;
-      HIP_CHECK(hipEventElapsedTime(&ms, ev_[j], ev_[j + 1]));
-      si.dispatch_ms += ms;
+      HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+      si.dispatch_ms = ms;
     }
     si.dispatches = enq;
     for (; k < enq; ++k) {
@@ -972,12 +999,15 @@ class SearchDeviceImpl : public SearchDevice {
       ++ran;
       si.processed += c[dev::HC_NIN];
       float ms = 0;
-      HIP_CHECK(hipEventElapsedTime(&ms, ev_[k], ev_[k + 1]));
-      ms_sum += ms;
+      if (trace_) {
+        HIP_CHECK(hipEventElapsedTime(&ms, ev_[k], ev_[k + 1]));
+        ms_sum += ms;
+      }
       if (trace_)
         std::fprintf(stderr, "[qi]     launch %u: in %u out %u halt %u, %.1f us\n", k, c[dev::HC_NIN], c[dev::HC_OUT],
                      c[dev::HC_HALT], ms * 1e3);
     }
+    if (!trace_) ms_sum = si.dispatch_ms;  // the chain's kernels back to back (<= 2 empty launches at its end)
     n_ = n_next;
     cur_ = cur_next;
     lc.used = log_next;

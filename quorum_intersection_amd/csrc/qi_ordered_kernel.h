@@ -349,6 +349,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
       cc[C_STOP] = 1u;
       a.host_ctr[HC_STOP] = 1u;
       a.host_ctr[HC_DONE] = 1u;
+      publish_flag(a.host_ctr, true, 0u);
     }
     return;
   }
@@ -375,6 +376,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
         a.host_ctr[HC_LOGB] = log_base;
         a.host_ctr[HC_STOP] = stop ? 1u : 0u;
         a.host_ctr[HC_DONE] = 1u;
+        publish_flag(a.host_ctr, stop, 0u);
       }
     }
     if (stop || blockIdx.x >= nb_used) return;
@@ -818,6 +820,7 @@ __device__ __forceinline__ void ordered_body(const OrdArgs& oa) {
         a.host_ctr[HC_LOGB] = log_base;
         a.host_ctr[HC_STOP] = 0u;
         a.host_ctr[HC_DONE] = 1u;
+        publish_flag(a.host_ctr, false, out);
       }
     }
   }

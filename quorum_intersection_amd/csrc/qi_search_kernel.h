@@ -271,6 +271,10 @@ enum : int {
   CTR_WORDS = 64,
   HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6,
   HC_BEST = 8,     // u64 (two words): the device-side best key after this launch
+  HC_FLAG = 10,    // u64, ONE 8-byte store, written last: bit 63 = published, bit 62 = stopped,
+                   // low 32 bits = units out.  The host spins on it in pinned memory to pace
+                   // its look-ahead (no event per launch); the other words are read after
+                   // the chain's final stream synchronisation.
   HC_WORDS = 16
 };
 // Output capacity per launch: n_in (carried-over units) + per used lane SPILL_RESERVE(S)
@@ -282,6 +286,11 @@ enum : int {
 __host__ __device__ constexpr uint32_t spill_reserve(uint32_t smax) { return smax + 4u; }
 constexpr int TOT_SHARDS = 64;  // running totals: [TOT_SHARDS][16] u64, shard = block % 64
 
+__device__ __forceinline__ void publish_flag(uint32_t* host_ctr, bool stop, uint32_t out) {
+  __hip_atomic_store((unsigned long long*)(host_ctr + HC_FLAG),
+                     (1ull << 63) | (stop ? (1ull << 62) : 0ull) | (unsigned long long)out, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
 constexpr int POLL_REPS = 64;
 constexpr int KEY_WORDS_MAX = 32;  // path-key words of the largest kernel shape (MW <= 32)
 struct SearchArgs {
@@ -548,6 +557,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       cc[C_STOP] = 1u;
       a.host_ctr[HC_STOP] = 1u;
       a.host_ctr[HC_DONE] = 1u;
+      publish_flag(a.host_ctr, true, 0u);
     }
     return;
   }
@@ -580,6 +590,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         a.host_ctr[HC_LOGB] = log_base;
         a.host_ctr[HC_STOP] = stop ? 1u : 0u;
         a.host_ctr[HC_DONE] = 1u;
+        publish_flag(a.host_ctr, stop, 0u);
       }
     }
     if (stop || blockIdx.x >= nb_used) return;
@@ -1496,6 +1507,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         a.host_ctr[HC_LOGB] = log_base;
         a.host_ctr[HC_STOP] = 0u;
         a.host_ctr[HC_DONE] = 1u;
+        publish_flag(a.host_ctr, false, out);
       }
     }
   }
