@@ -266,8 +266,8 @@ enum : int {
   C_HALT = 37,     // 1: this launch carried units over (its lanes ran out of budget with
                    // units left); the rest of the chain does nothing and the host sorts
                    // the frontier into preorder before it goes on
-  C_PEAKED = 38,   // 1: this or an earlier launch of the chain ran with the run budget: the
-                   // frontier has covered the lanes once, what follows is its decay
+  C_PEAKED = 38,   // launches of the chain so far that ran with the run budget (> 0: the
+                   // frontier has covered the lanes once, what follows is its decay)
   CTR_WORDS = 64,
   HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6,
   HC_BEST = 8,     // u64 (two words): the device-side best key after this launch
@@ -569,7 +569,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   const uint64_t spill_need = (uint64_t)n_in + (uint64_t)nb_used * WAVE * spill_reserve(SMAX);
   const uint32_t evict_pool = spill_need < (uint64_t)a.out_cap ? (uint32_t)((uint64_t)a.out_cap - spill_need) : 0u;
   // (QI_DECAY_RUN 2: not once a witness is known -- short launches then prune sooner)
-  const bool peaked_in = QI_DECAY_RUN && pc[C_PEAKED] != 0u && (QI_DECAY_RUN == 1 || *a.best64 == ~0ull);
+  const uint32_t peaked_n = pc[C_PEAKED];  // run-budget launches of this chain so far
+  const bool peaked_in = QI_DECAY_RUN && peaked_n != 0u && (QI_DECAY_RUN == 1 || *a.best64 == ~0ull);
   const uint32_t budget = launch_budget(a, n_in, peaked_in);
   {
     // the final spills, and at least evict_max evictions per used lane
@@ -581,7 +582,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       cc[C_LOGB] = log_base;
       cc[C_STATIC] = static_end;
       cc[C_STOP] = stop ? 1u : 0u;
-      cc[C_PEAKED] = (peaked_in || (!stop && nb_used != 0 && budget == a.run_budget)) ? 1u : 0u;
+      cc[C_PEAKED] = peaked_n + ((!stop && nb_used != 0 && budget == a.run_budget) ? 1u : 0u);
       if (stop || nb_used == 0) {  // nothing runs: publish now (else the last block does)
         cc[C_LOGN] = log_base;
         a.host_ctr[HC_LOGN] = log_base;
