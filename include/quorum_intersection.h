@@ -50,6 +50,11 @@ int qi_device_count(void);
  * first device call would otherwise pay); *ms = wall time.  Lets a caller report device
  * init apart from time-to-verdict. */
 int qi_device_warmup(int device, double* ms);
+/* With QI_TIMING set in the environment: the phase times of this process so far as a JSON
+ * object ({"parse_ms": .., "graph_scc_ms": .., "flatten_global_ms": .., "gfp_device_setup_ms":
+ * .., "scc_checks_ms": .., "flatten_local_ms": .., "search_engine_setup_ms": .., "search_ms":
+ * .., "search_kernels_ms": ..}); "{}" otherwise.  Valid until the thread's next call. */
+const char* qi_timing_json(void);
 
 /* ---------------------------------------------------------------------------------
  * FBAS: parseStellarConfigurationJSON + buildDependencyGraph + strong_components
@@ -84,8 +89,8 @@ int qi_gfp_batch(qi_fbas* f, const uint64_t* nodes, const uint64_t* avail, uint3
  * threshold node) and a counter header live in a fixed array of QI_STATIC_SCRATCH_BYTES
  * that the library holds on every GPU it runs on until the process ends; the call makes no
  * hipMalloc / hipFree / hipHostMalloc and no other allocating call.  `stream`: a
- * hipStream_t to enqueue on without synchronising, or NULL to run on the library's stream
- * and wait.  Set-up is not part of it: the qi_fbas must have run qi_gfp_batch or qi_solve
+ * hipStream_t to enqueue on without synchronising, or NULL to run on HIP's default stream
+ * of that device and wait.  Set-up is not part of it: the qi_fbas must have run qi_gfp_batch or qi_solve
  * once (that uploads the threshold-node tables), else QI_ERR_STATE.  count queries whose
  * state exceeds the array: QI_ERR_CAPACITY (split the batch).  Every call on a GPU uses
  * that GPU's one array: calls that overlap on one GPU (other threads, other streams) race. */

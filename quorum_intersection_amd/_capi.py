@@ -102,6 +102,7 @@ SIGNATURES = {
     "qi_abi_version": (c_int, []),
     "qi_device_count": (c_int, []),
     "qi_device_warmup": (c_int, [c_int, POINTER(c_double)]),
+    "qi_timing_json": (c_char_p, []),
     "qi_fbas_from_json": (c_int, [c_char_p, c_size_t, c_int, POINTER(c_void_p)]),
     "qi_fbas_destroy": (None, [c_void_p]),
     "qi_fbas_num_vertices": (c_uint32, [c_void_p]),

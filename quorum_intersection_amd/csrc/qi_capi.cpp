@@ -55,7 +55,11 @@ struct qi_fbas {
     if (!gfp) {
       if (qi::device_count() <= device || device < 0)
         throw qi::Error(QI_ERR_DEVICE, "no HIP device " + std::to_string(device) + " (the MI355X path has no CPU fallback)");
-      if (!gflat) gflat.reset(new qi::GlobalFlat(qi::flatten_global(g)));
+      if (!gflat) {
+        qi::timing::Scope t("flatten_global");
+        gflat.reset(new qi::GlobalFlat(qi::flatten_global(g)));
+      }
+      qi::timing::Scope t("gfp_device_setup");
       gfp = qi::make_gfp_device(device, *gflat);
     }
     return *gfp;
@@ -81,7 +85,11 @@ std::vector<uint32_t> scc_quorum_check(qi_fbas* f, std::vector<std::vector<uint3
   std::vector<uint64_t> masks((size_t)C * W, 0), out((size_t)C * W, 0);
   for (uint32_t c = 0; c < C; ++c)
     for (uint32_t v : f->sccs.members[c]) masks[(size_t)c * W + v / 64] |= 1ull << (v % 64);
-  f->gfp_dev().run(masks.data(), masks.data(), C, out.data());
+  {
+    qi::GfpDevice& gd = f->gfp_dev();
+    qi::timing::Scope t("scc_checks");
+    gd.run(masks.data(), masks.data(), C, out.data());
+  }
   for (uint32_t c = 0; c < C; ++c) {
     bool any = false;
     std::vector<uint32_t> q;
@@ -140,11 +148,18 @@ const char* qi_last_error(void) { return g_err.c_str(); }
 int qi_abi_version(void) { return QI_ABI_VERSION; }
 int qi_device_count(void) { return qi::device_count(); }
 
+const char* qi_timing_json(void) {
+  thread_local std::string s;
+  s = qi::timing::json();
+  return s.c_str();
+}
+
 int qi_device_warmup(int device, double* ms) {
   return guarded([&] {
     auto t0 = std::chrono::steady_clock::now();
     if (qi::device_count() <= device || device < 0) throw qi::Error(QI_ERR_DEVICE, "no HIP device " + std::to_string(device));
     qi::device_free(device, qi::device_alloc(device, 64));
+    qi::device_prepare(device);  // the first stream (hardware queue) and the library's code object
     if (ms) *ms = ms_since(t0);
     return QI_OK;
   });
@@ -154,8 +169,16 @@ int qi_fbas_from_json(const char* json, size_t len, int device, qi_fbas** out) {
   if (!json || !out) return fail(QI_ERR_ARG, "null argument");
   return guarded([&] {
     std::unique_ptr<qi_fbas> f(new qi_fbas);
-    f->g = qi::build_graph(qi::parse_stellar_json(json, len));
-    f->sccs = qi::strong_components(f->g);
+    std::vector<qi::StellarNode> nodes;
+    {
+      qi::timing::Scope t("parse");
+      nodes = qi::parse_stellar_json(json, len);
+    }
+    {
+      qi::timing::Scope t("graph_scc");
+      f->g = qi::build_graph(nodes);
+      f->sccs = qi::strong_components(f->g);
+    }
     f->device = device;
     for (const auto& a : f->g.adj) f->edges += (uint32_t)a.size();
     *out = f.release();

@@ -21,7 +21,7 @@ class GfpDevice {
   // The same fixpoints for callers that cannot allocate: masks in DEVICE memory, per-query
   // state in the library's fixed device scratch array (QI_STATIC_SCRATCH_BYTES per GPU, shared
   // by every call on that GPU), no hipMalloc / hipFree / hipHostMalloc.  stream = a
-  // hipStream_t to enqueue on (no synchronisation), or null: the engine's own stream, waited
+  // hipStream_t to enqueue on (no synchronisation), or null: HIP's default stream, waited
   // for before returning.  Throws QI_ERR_CAPACITY when count queries do not fit the array.
   virtual void run_static(const uint64_t* d_nodes, const uint64_t* d_avail, uint32_t count, uint64_t* d_out,
                           void* stream) = 0;
@@ -138,6 +138,11 @@ bool jit_precompile(const LocalFlat& f, std::string* log);
 
 int device_count();
 int device_cu_count(int device);
+// Device initialisation beyond the context: creates the first pooled stream (the first
+// hardware queue of a process costs ~9 ms) and loads the library's base code object (the
+// batched fixpoint kernels and the static scratch array).  Optional; the first device call
+// pays for it otherwise.
+void device_prepare(int device);
 
 // Device memory for frontier hand-offs between engines (qi_shard.cpp): units move
 // device-to-device, across GPUs over xGMI with hipMemcpyPeerAsync.

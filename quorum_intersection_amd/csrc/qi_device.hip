@@ -397,6 +397,17 @@ bool enable_peer(int a, int b) {
 
 namespace {
 
+// Stack levels of the run-time specialised kernel for a template shape.  |SCC| <= 32: 20
+// levels leave LDS for 9 resident waves per CU instead of 8 (17,408 B per wave).  Measured
+// on the bench workload: 24 / 22 / 21 / 20 / 19 / 14 levels = 8 / 8 / 8 / 9 / 9 / 12 waves gave
+// 2.63 / 2.62 / 2.55 / 2.39 / 2.38 / 2.48 ms; below 19 the extra stack evictions cost more
+// than the waves bring.  The engine and jit_precompile must agree (the cache key is the source).
+inline int jit_default_smax(int MW, int SMAX) {
+  int s = MW == 1 ? 20 : SMAX;
+  if (const char* e = std::getenv("QI_JIT_SMAX")) s = std::max(4, std::min(64, std::atoi(e)));  // diagnostics
+  return s;
+}
+
 // hipStreamCreate costs ~2 ms on this stack (measured, QI_TRACE): engines take their stream
 // from a per-device pool and return it, so a solve does not pay it twice.
 struct StreamPool {
@@ -463,10 +474,23 @@ class GfpDeviceImpl : public GfpDevice {
  public:
   GfpDeviceImpl(int device, const GlobalFlat& g) : device_(device) {
     DeviceGuard dg(device_);
+    auto tc0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+      if (!timing::enabled()) return;
+      const auto now = std::chrono::steady_clock::now();
+      timing::add((std::string("gfp_") + what).c_str(), std::chrono::duration<double, std::milli>(now - tc0).count());
+      tc0 = now;
+    };
     static_ = static_scratch_ptr(device_);  // set-up: this device's scratch array address
+    lap("scratch_symbol");
+    // the stream goes back to the per-device pool after set-up and after every run(), so the
+    // search engine of the same solve reuses it (a stream costs ~2 ms to create, the first
+    // one of a process ~9 ms)
     stream_ = acquire_stream(device_);
+    lap("stream");
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
+    lap("events");
     d_.n = g.n;
     d_.words = g.words;
     d_.T = g.T;
@@ -482,7 +506,11 @@ class GfpDeviceImpl : public GfpDevice {
     bufs_.push_back(d_.cref = dupload(g.cref, stream_));
     bufs_.push_back(d_.root = dupload(g.root, stream_));
     rounds_ = dalloc<unsigned long long>(1);
+    lap("alloc_upload");
     HIP_CHECK(hipStreamSynchronize(stream_));
+    release_stream(device_, stream_);
+    stream_ = nullptr;
+    lap("sync");
   }
   ~GfpDeviceImpl() override {
     DeviceGuard dg(device_);
@@ -495,9 +523,18 @@ class GfpDeviceImpl : public GfpDevice {
     (void)hipEventDestroy(e1_);
     release_stream(device_, stream_);
   }
+  struct StreamLease {  // the engine's stream for the duration of one call
+    GfpDeviceImpl& g;
+    explicit StreamLease(GfpDeviceImpl& g_) : g(g_) { g.stream_ = acquire_stream(g.device_); }
+    ~StreamLease() {
+      release_stream(g.device_, g.stream_);
+      g.stream_ = nullptr;
+    }
+  };
   void run(const uint64_t* nodes, const uint64_t* avail, uint32_t count, uint64_t* out) override {
     if (count == 0) return;
     DeviceGuard dg(device_);
+    StreamLease lease(*this);
     const size_t per = (size_t)count * d_.words;
     if (io_cap_ < per) {
       (void)hipFree(io_);
@@ -561,14 +598,16 @@ class GfpDeviceImpl : public GfpDevice {
         throw Error(QI_ERR_ARG, "qi_gfp_batch_static: masks must be device memory of HIP device " + std::to_string(device_));
       }
     }
-    hipStream_t s = stream ? (hipStream_t)stream : stream_;
+    // no caller stream: HIP's default stream of this device (creating or borrowing a stream
+    // of the library's pool could allocate)
+    hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t) nullptr;
     unsigned long long* rounds = (unsigned long long*)static_;
     hipLaunchKernelGGL(dev::zero_u64_kernel, dim3(1), dim3(64), 0, s, rounds, (uint32_t)(kStaticScratchHeader / 8));
     hipLaunchKernelGGL(dev::gfp_batch_kernel<true>, dim3(count), dim3(64), 0, s, d_,
                        (const unsigned long long*)d_nodes, (const unsigned long long*)d_avail, count,
                        (unsigned long long*)d_out, rounds, (uint8_t*)(static_ + kStaticScratchHeader), per);
     HIP_CHECK(hipGetLastError());
-    if (!stream) HIP_CHECK(hipStreamSynchronize(stream_));
+    if (!stream) HIP_CHECK(hipStreamSynchronize(nullptr));
   }
   double last_kernel_ms() const override { return last_ms_; }
 
@@ -608,10 +647,11 @@ class SearchDeviceImpl : public SearchDevice {
     trace_ = std::getenv("QI_TRACE") != nullptr;
     auto tc0 = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
-      if (!trace_) return;
+      if (!trace_ && !timing::enabled()) return;
       const auto now = std::chrono::steady_clock::now();
-      std::fprintf(stderr, "[qi]   ctor %-22s %.3f ms\n", what,
-                   std::chrono::duration<double, std::milli>(now - tc0).count());
+      const double ms = std::chrono::duration<double, std::milli>(now - tc0).count();
+      if (trace_) std::fprintf(stderr, "[qi]   ctor %-22s %.3f ms\n", what, ms);
+      timing::add((std::string("engine_") + what).c_str(), ms);
       tc0 = now;
     };
     // tuning overrides for experiments (profiling only; defaults are the measured best)
@@ -620,13 +660,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
-    jit_smax_ = SMAX;
-    // |SCC| <= 32: 20 stack levels leave LDS for 9 resident waves per CU instead of 8
-    // (17,408 B per wave).  Measured on the bench workload: 24 / 22 / 21 / 20 / 19 / 14 levels
-    // = 8 / 8 / 8 / 9 / 9 / 12 waves gave 2.63 / 2.62 / 2.55 / 2.39 / 2.38 / 2.48 ms; below 19
-    // the extra stack evictions cost more than the waves bring.
-    if (MW == 1 && !ORD) jit_smax_ = 20;
-    if (const char* e = std::getenv("QI_JIT_SMAX")) jit_smax_ = std::max(4, std::min(64, std::atoi(e)));
+    jit_smax_ = ORD ? SMAX : jit_default_smax(MW, SMAX);
     if (ORD) cfg_.jit = 1;  // no run-time specialisation of the ordered kernel
     stream_ = acquire_stream(device_);
     HIP_CHECK(hipEventCreate(&e0_));
@@ -727,22 +761,9 @@ class SearchDeviceImpl : public SearchDevice {
       jit_shm_ -= (ow_full - owl) * 64 * 4;
     }
     jit_shm_ = (jit_shm_ + 15) / 16 * 16;
-    const void* kfn;
-    if constexpr (ORD) kfn = (const void*)dev::ordered_kernel<MW, TW>;
-    else kfn = (const void*)dev::search_kernel<MW, TW, SMAX>;
-    if (!ORD) HIP_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
-    if (!cfg_.max_blocks) {  // one resident wave of blocks: no second-wave tail
-      int nb = 0;
-      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 64, shm_));
-      if (ORD) nb = std::min(nb, 8);  // scratch-heavy lanes: a few waves per CU hide the latency
-      if (nb > 0) max_blocks_ = cus_ * (uint32_t)nb;
-    }
-    if (ORD) {  // one DFS stack (and, beyond 256 vertices, one workspace) per lane of a launch
-      keep(ord_.ostack = dalloc<uint32_t>((size_t)max_blocks_ * kOrdSmax * (dev::OrdUnitLayout<MW>::OWT + 3) * 64));
-      if (dev::OrdWorkspace<MW>::GLOBAL)
-        keep(ord_.ows = dalloc<uint8_t>((size_t)max_blocks_ * 64 * dev::OrdWorkspace<MW>::BYTES));
-    }
-    lap("occupancy");
+    // The ahead-of-time kernel's attributes and occupancy are looked up when it is first
+    // needed (aot_setup): touching it loads its code object (~6 ms), which a search that
+    // runs the cached specialised kernel from its first launch never pays.
     if ((cfg_.jit == 0 || cfg_.jit == 4) && jit_eligible(flat_)) {
       // auto / cache-only: a specialised kernel already in the on-disk cache runs from the
       // first launch (hipModuleLoadData, ~1 ms); auto compiles a missing one in the
@@ -758,6 +779,8 @@ class SearchDeviceImpl : public SearchDevice {
       if (!wait_jit()) throw Error(QI_ERR_UNSUPPORTED, "specialised kernel failed to build: " + jit_log_);
     }
     lap("jit");
+    if (ORD || !jit_fn_) aot_setup();
+    lap("aot_kernel");
     reset_root();
     lap("root");
   }
@@ -829,6 +852,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (cfg_.jit == 0 && launches_ >= cfg_.jit_after && jit_state_.load() == 0 && jit_eligible(flat_)) start_jit();
     if (jit_state_.load() == 2) load_jit();
     const bool spec = jit_fn_ != nullptr;
+    if (!spec) aot_setup();
     const uint32_t smax = ORD ? kOrdSmax : (spec ? (uint32_t)jit_smax_ : (uint32_t)SMAX);
     const uint32_t blocks = max_blocks_;
     const uint32_t K = std::max(1u, std::min(cfg_.batch ? cfg_.batch : (uint32_t)kMaxBatch, (uint32_t)kMaxBatch));
@@ -840,6 +864,7 @@ class SearchDeviceImpl : public SearchDevice {
       return n + nb * 64u * (dev::spill_reserve(smax) + cfg_.evict_max);  // search_body's need_out
     };
     {
+      timing::Scope tsc("frontier_alloc");
       const uint64_t need = first_need(n_);
       if (need > 0xFFFFFFF0ull) throw Error(QI_ERR_CAPACITY, "search frontier exceeds 2^32 units");
       ensure_cap(cur_, need, true);
@@ -1012,6 +1037,7 @@ class SearchDeviceImpl : public SearchDevice {
     cur_ = cur_next;
     lc.used = log_next;
     if (stopped) {
+      timing::Scope tsc("frontier_alloc");
       const uint64_t need = first_need(n_);
       if (need > 0xFFFFFFF0ull) throw Error(QI_ERR_CAPACITY, "search frontier exceeds 2^32 units");
       if (need > std::min(cap_[0], cap_[1])) {  // grow once to the full-grid bound (ramp stops
@@ -1422,6 +1448,32 @@ class SearchDeviceImpl : public SearchDevice {
     });
   }
 
+  // Attributes, occupancy (and the ordered kernel's per-lane stacks) of the ahead-of-time
+  // kernel; once, before its first launch.
+  void aot_setup() {
+    if (aot_ready_) return;
+    aot_ready_ = true;
+    DeviceGuard dg(device_);
+    const void* kfn;
+    if constexpr (ORD) kfn = (const void*)dev::ordered_kernel<MW, TW>;
+    else kfn = (const void*)dev::search_kernel<MW, TW, SMAX>;
+    if (!ORD) HIP_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
+    if (!cfg_.max_blocks) {  // one resident wave of blocks: no second-wave tail
+      int nb = 0;
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 64, shm_));
+      if (ORD) nb = std::min(nb, 8);  // scratch-heavy lanes: a few waves per CU hide the latency
+      if (nb > 0) aot_blocks_ = cus_ * (uint32_t)nb;
+    }
+    if (!jit_fn_) max_blocks_ = aot_blocks_ ? aot_blocks_ : max_blocks_;
+    if (ORD) {  // one DFS stack (and, beyond 256 vertices, one workspace) per lane of a launch
+      keep(ord_.ostack = dalloc<uint32_t>((size_t)max_blocks_ * kOrdSmax * (dev::OrdUnitLayout<MW>::OWT + 3) * 64));
+      if (dev::OrdWorkspace<MW>::GLOBAL)
+        keep(ord_.ows = dalloc<uint8_t>((size_t)max_blocks_ * 64 * dev::OrdWorkspace<MW>::BYTES));
+    }
+  }
+  bool aot_ready_ = false;
+  uint32_t aot_blocks_ = 0;
+
   void load_jit() {
     if (jit_state_.load() != 2) return;
     if (jit_thread_.joinable()) jit_thread_.join();
@@ -1501,6 +1553,12 @@ uint32_t hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint3
 }
 
 
+void device_prepare(int device) {
+  DeviceGuard dg(device);
+  release_stream(device, acquire_stream(device));
+  (void)static_scratch_ptr(device);
+}
+
 std::unique_ptr<GfpDevice> make_gfp_device(int device, const GlobalFlat& g) {
   if (const char* e = std::getenv("QI_GFP_LDS")) GfpDeviceImpl::kLdsImage = (size_t)std::atoll(e);
   return std::unique_ptr<GfpDevice>(new GfpDeviceImpl(device, g));
@@ -1519,7 +1577,7 @@ bool jit_precompile(const LocalFlat& f, std::string* log) {
   else if (mw <= 8 && tw <= 8) { MW = 8; TW = 8; SMAX = 8; }
   else return false;
   if (!jit_eligible(f)) return false;
-  return !jit_compile(jit_source(f, MW, TW, SMAX, false), log).empty();
+  return !jit_compile(jit_source(f, MW, TW, jit_default_smax(MW, SMAX), false), log).empty();
 }
 
 std::unique_ptr<SearchDevice> make_search_device(int device, const LocalFlat& f, const SearchConfig& cfg) {

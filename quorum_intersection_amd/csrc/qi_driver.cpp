@@ -113,13 +113,19 @@ SearchOutcome search_front_scc(const Graph& g, const std::vector<uint32_t>& scc,
   auto t0 = std::chrono::steady_clock::now();
   LocalFlat lf = flatten_local(g, scc);
   auto t1 = std::chrono::steady_clock::now();
+  timing::add("flatten_local", ms_since(t0));
   auto sd = make_search_device(device, lf, cfg);
   auto t2 = std::chrono::steady_clock::now();
+  timing::add("search_engine_setup", ms_since(t1));
   int steps = 0;
   while (sd->frontier_size()) {  // step() throws QI_ERR_STATE on repeated no-progress steps
     sd->step(0);
     ++steps;
   }
+  timing::add("search", ms_since(t2));
+  timing::add("search_kernels", sd->sum_kernel_ms());
+  timing::count("search_launches", (double)sd->launches());
+  timing::count("search_specialised_launches", (double)sd->specialized_launches());
   if (trace)
     std::fprintf(stderr, "[qi] flatten %.3f ms, create %.3f ms, %d steps %.3f ms\n", ms_since(t0) - ms_since(t1),
                  ms_since(t1) - ms_since(t2), steps, ms_since(t2));

@@ -19,6 +19,25 @@ struct Error : std::runtime_error {
 };
 
 // ----------------------------------------------------------------------------------
+// Phase times of the drop-in's time-to-verdict (QI_TIMING): parse, graph + SCCs, flatten,
+// device set-up, per-SCC checks, search, text.  Process-wide, filled by every stage when
+// enabled, read once by the CLI (qi_timing_json).
+// ----------------------------------------------------------------------------------
+namespace timing {
+bool enabled();                          // QI_TIMING is set
+void add(const char* phase, double ms);  // accumulates per phase name, in first-use order
+void count(const char* name, double n);  // a plain number beside the phases (no "_ms" suffix)
+std::string json();                      // {"phase_ms": value, ...}
+struct Scope {                           // adds its lifetime to `phase` (no-op when disabled)
+  const char* phase;
+  bool on;
+  long long t0;
+  explicit Scope(const char* p);
+  ~Scope();
+};
+}  // namespace timing
+
+// ----------------------------------------------------------------------------------
 // Ingestion (cpp:402-436): boost::property_tree keeps every scalar as text.
 // ----------------------------------------------------------------------------------
 struct QuorumSetIds {               // GenericQuorumSet<NodeID>

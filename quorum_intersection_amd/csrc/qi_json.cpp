@@ -263,3 +263,62 @@ std::vector<StellarNode> parse_stellar_json(const char* text, size_t len) {
 }
 
 }  // namespace qi
+
+// ----------------------------------------------------------------------------------
+// Phase timing (qi_internal.h, namespace timing)
+// ----------------------------------------------------------------------------------
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <utility>
+
+namespace qi {
+namespace timing {
+namespace {
+std::mutex g_mu;
+std::vector<std::pair<std::string, double>> g_phases;
+long long now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+bool enabled() {
+  static const bool on = std::getenv("QI_TIMING") != nullptr;
+  return on;
+}
+
+namespace {
+void accumulate(const std::string& key, double v) {
+  if (!enabled()) return;
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto& p : g_phases)
+    if (p.first == key) {
+      p.second += v;
+      return;
+    }
+  g_phases.emplace_back(key, v);
+}
+}  // namespace
+
+void add(const char* phase, double ms) { accumulate(std::string(phase) + "_ms", ms); }
+void count(const char* name, double n) { accumulate(name, n); }
+
+std::string json() {
+  std::lock_guard<std::mutex> g(g_mu);
+  std::string o = "{";
+  char buf[64];
+  for (size_t i = 0; i < g_phases.size(); ++i) {
+    std::snprintf(buf, sizeof buf, "%.3f", g_phases[i].second);
+    o += (i ? ", \"" : "\"") + g_phases[i].first + "\": " + buf;
+  }
+  return o + "}";
+}
+
+Scope::Scope(const char* p) : phase(p), on(enabled()), t0(on ? now_ns() : 0) {}
+Scope::~Scope() {
+  if (on) add(phase, (double)(now_ns() - t0) * 1e-6);
+}
+}  // namespace timing
+}  // namespace qi
+

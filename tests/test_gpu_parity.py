@@ -314,6 +314,29 @@ def test_cli_binary_verdicts_and_exit_codes():
         assert r.stdout.decode() == Oracle().load(fixture_text(name)).solve_text(True, False)
 
 
+def test_cli_second_run_uses_the_cached_specialised_kernel(tmp_path):
+    # The drop-in compiles nothing before the verdict: the first run on a network searches
+    # with the table-interpreting kernel and fills the on-disk cache afterwards; the second
+    # run loads the specialised kernel from it (the engine and the fill must agree on the
+    # generated source, stack depth included).  QI_TIMING reports the phases.
+    import subprocess
+    exe = os.path.join(ROOT, "bin", "quorum_intersection")
+    text = fbas_gen.two_tier(7, 64).encode()
+    env = dict(os.environ, QI_TIMING="1", QI_JIT_CACHE=str(tmp_path / "cache"))
+    runs = []
+    for _ in range(2):
+        r = subprocess.run([exe], input=text, capture_output=True, env=env)
+        assert (r.stdout, r.returncode) == (b"true\n", 0)
+        runs.append(json.loads(r.stderr.decode().strip().splitlines()[-1]))
+    cold, warm = (x["phases"] for x in runs)
+    assert cold["search_launches"] > 0 and cold["search_specialised_launches"] == 0
+    assert warm["search_specialised_launches"] == warm["search_launches"] > 0
+    for key in ("parse_ms", "graph_scc_ms", "flatten_global_ms", "gfp_device_setup_ms", "scc_checks_ms",
+                "flatten_local_ms", "search_engine_setup_ms", "search_ms", "search_kernels_ms"):
+        assert key in warm, key
+    assert runs[1]["stdin_to_verdict_ms"] > 0 and runs[1]["device_init_ms"] > 0
+
+
 def test_cli_threshold_minus_one_matches_oracle():
     # "threshold": "-1" wraps to SIZE_MAX (never satisfiable); the drop-in CLI and the
     # oracle CLI agree byte for byte on the verdict and the -v text
