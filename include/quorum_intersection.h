@@ -29,15 +29,23 @@ enum {
   QI_ERR_PARSE = 1,       /* JSON / schema error: the reference throws ptree_error and aborts */
   QI_ERR_DEVICE = 2,      /* HIP runtime error, or no GPU: the product never falls back to CPU */
   QI_ERR_ARG = 3,
-  QI_ERR_UNSUPPORTED = 4, /* searched SCC beyond the compiled kernel shapes (|SCC| > 256) */
+  QI_ERR_UNSUPPORTED = 4, /* the one input class the drop-in refuses: a searched SCC (sccs.front())
+                             of more than 1024 vertices or more than 1024 distinct threshold
+                             nodes (the largest compiled kernel shape); the reference searches
+                             any size (plain vectors, cpp:140-346) */
   QI_ERR_CAPACITY = 5,
   QI_ERR_STATE = 6
 };
 
 /* findBestNode tie-break (cpp:203-250).  The reference samples uniformly among the
  * maximal in-degree vertices; QI_TIE_LOWEST picks the lowest vertex index of that set,
- * which is one of the reference's possible executions and makes counts reproducible. */
-enum { QI_TIE_LOWEST = 0 };
+ * which is one of the reference's possible executions and makes counts reproducible.
+ * QI_TIE_RANDOM is the reference's own rule with a reproducible draw: uniform over the
+ * maximal in-degree vertices of Q \ D, drawn from a hash of (qi_solve_opts.tie_seed, the
+ * node's path, its depth) instead of a process-global engine (cpp:207).  Verdicts do not
+ * depend on the rule; node counts and, on early exits, the witness do.  Not available for
+ * SCCs with threshold-0 quorum sets or beyond 256 vertices (QI_ERR_UNSUPPORTED). */
+enum { QI_TIE_LOWEST = 0, QI_TIE_RANDOM = 1 };
 
 typedef struct qi_fbas qi_fbas;
 typedef struct qi_search qi_search;
@@ -104,7 +112,7 @@ int qi_gfp_batch_static(qi_fbas* f, const uint64_t* d_nodes, const uint64_t* d_a
  * search on sccs.front() (checkMinimalQuorums, cpp:348-400 / 691) on the GPU.
  * ------------------------------------------------------------------------------- */
 typedef struct {
-  uint32_t tiebreak;       /* QI_TIE_LOWEST */
+  uint32_t tiebreak;       /* QI_TIE_LOWEST or QI_TIE_RANDOM */
   uint32_t grow_budget;    /* 0 = default: per-lane node budget while the frontier grows */
   uint32_t run_budget;     /* 0 = default: per-lane node budget at full occupancy */
   uint32_t max_blocks;     /* 0 = default (8 wavefronts per CU) */
@@ -122,6 +130,7 @@ typedef struct {
   uint32_t device_mask;    /* HIP devices of the search, bit d = device d; 0 = the qi_fbas
                               device only.  Units move between devices over xGMI
                               (hipMemcpyPeerAsync) */
+  uint32_t tie_seed;       /* QI_TIE_RANDOM: seed of the draws */
 } qi_solve_opts;
 
 typedef struct {

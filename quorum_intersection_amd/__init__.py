@@ -132,12 +132,14 @@ class FBAS:
 
     # ---- device: solve / search -------------------------------------------------------
     def solve_stats(self, grow_budget: int = 0, run_budget: int = 0, max_blocks: int = 0, jit: int = 0,
-                    batch: int = 0, engines: int = 0, device_mask: int = 0) -> Dict:
+                    batch: int = 0, engines: int = 0, device_mask: int = 0, tiebreak: int = 0,
+                    tie_seed: int = 0) -> Dict:
         """jit: 0 auto (specialised kernel compiled in the background for long searches),
         1 table-interpreting kernel only, 2 specialised kernel from the first launch.
         engines / device_mask: sharded search over several engines (one host thread and
         HIP stream each) on the devices of device_mask (0 = this FBAS's device)."""
-        opts = _capi.SolveOpts(0, grow_budget, run_budget, max_blocks, jit, batch, engines, device_mask)
+        # tiebreak: 0 lowest vertex index, 1 the reference's uniform draw (seeded with tie_seed)
+        opts = _capi.SolveOpts(tiebreak, grow_budget, run_budget, max_blocks, jit, batch, engines, device_mask, tie_seed)
         res = _capi.SolveResult()
         q1 = np.zeros(max(self.n, 1), dtype=np.uint32)
         q2 = np.zeros(max(self.n, 1), dtype=np.uint32)

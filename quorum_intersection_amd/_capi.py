@@ -29,7 +29,8 @@ class QIError(RuntimeError):
 
 class SolveOpts(ctypes.Structure):
     _fields_ = [("tiebreak", c_uint32), ("grow_budget", c_uint32), ("run_budget", c_uint32), ("max_blocks", c_uint32),
-                ("jit", c_uint32), ("batch", c_uint32), ("engines", c_uint32), ("device_mask", c_uint32)]
+                ("jit", c_uint32), ("batch", c_uint32), ("engines", c_uint32), ("device_mask", c_uint32),
+                ("tie_seed", c_uint32)]
 
 
 class SolveResult(ctypes.Structure):

@@ -106,8 +106,11 @@ std::vector<uint32_t> scc_quorum_check(qi_fbas* f, std::vector<std::vector<uint3
   return with;
 }
 
-qi::SearchConfig make_cfg(uint32_t grow, uint32_t run, uint32_t blocks, uint32_t jit = 0, uint32_t batch = 0) {
+qi::SearchConfig make_cfg(uint32_t grow, uint32_t run, uint32_t blocks, uint32_t jit = 0, uint32_t batch = 0,
+                          uint32_t tiebreak = 0, uint32_t tie_seed = 0) {
   qi::SearchConfig c;
+  c.tiebreak = tiebreak;
+  c.tie_seed = tie_seed;
   c.jit = jit;
   if (batch) c.batch = batch;
   if (grow) c.grow_budget = grow;
@@ -238,7 +241,7 @@ int qi_gfp_batch_static(qi_fbas* f, const uint64_t* d_nodes, const uint64_t* d_a
 
 int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32_t* q1, uint32_t* q2) {
   if (!f || !res) return fail(QI_ERR_ARG, "null argument");
-  if (opts && opts->tiebreak != QI_TIE_LOWEST) return fail(QI_ERR_UNSUPPORTED, "only QI_TIE_LOWEST is implemented");
+  if (opts && opts->tiebreak > QI_TIE_RANDOM) return fail(QI_ERR_ARG, "tiebreak: QI_TIE_LOWEST or QI_TIE_RANDOM");
   return guarded([&] {
     std::memset(res, 0, sizeof *res);
     res->n_vertices = f->g.n();
@@ -256,7 +259,8 @@ int qi_solve(qi_fbas* f, const qi_solve_opts* opts, qi_solve_result* res, uint32
     }
     res->searched = 1;
     qi::SearchConfig cfg = make_cfg(opts ? opts->grow_budget : 0, opts ? opts->run_budget : 0,
-                                    opts ? opts->max_blocks : 0, opts ? opts->jit : 0, opts ? opts->batch : 0);
+                                    opts ? opts->max_blocks : 0, opts ? opts->jit : 0, opts ? opts->batch : 0,
+                                    opts ? opts->tiebreak : 0, opts ? opts->tie_seed : 0);
     auto t1 = std::chrono::steady_clock::now();
     qi::SearchOutcome o = run_search(f, cfg, opts);
     res->t_search_ms = ms_since(t1);
@@ -290,7 +294,7 @@ int qi_solve_text(qi_fbas* f, int verbose, int graphviz, char** text, int* verdi
 
 int qi_solve_text_ex(qi_fbas* f, int verbose, int graphviz, const qi_solve_opts* opts, char** text, int* verdict) {
   if (!f || !text || !verdict) return fail(QI_ERR_ARG, "null argument");
-  if (opts && opts->tiebreak != QI_TIE_LOWEST) return fail(QI_ERR_UNSUPPORTED, "only QI_TIE_LOWEST is implemented");
+  if (opts && opts->tiebreak > QI_TIE_RANDOM) return fail(QI_ERR_ARG, "tiebreak: QI_TIE_LOWEST or QI_TIE_RANDOM");
   return guarded([&] {
     std::ostringstream out;
     const auto& S = f->sccs.members;
@@ -318,7 +322,8 @@ int qi_solve_text_ex(qi_fbas* f, int verbose, int graphviz, const qi_solve_opts*
       result = false;
     } else {
       qi::SearchConfig cfg = make_cfg(opts ? opts->grow_budget : 0, opts ? opts->run_budget : 0,
-                                      opts ? opts->max_blocks : 0, opts ? opts->jit : 0, opts ? opts->batch : 0);
+                                      opts ? opts->max_blocks : 0, opts ? opts->jit : 0, opts ? opts->batch : 0,
+                                    opts ? opts->tiebreak : 0, opts ? opts->tie_seed : 0);
       qi::SearchOutcome o = run_search(f, cfg, opts);
       if (o.found) {
         if (verbose) {

@@ -57,6 +57,10 @@ struct SearchConfig {
   // kernel; never compiles).  0 and 4 load a cached kernel before the first launch.
   uint32_t jit = 0;
   uint32_t jit_after = 3;
+  // findBestNode ties (cpp:229-246): 0 = lowest vertex index (reproducible counts), 1 = a
+  // seeded uniform draw over the maximal in-degree vertices, the reference's own rule
+  uint32_t tiebreak = 0;
+  uint32_t tie_seed = 0;
 };
 
 struct StepInfo {

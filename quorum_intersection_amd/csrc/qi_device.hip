@@ -662,6 +662,10 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
     jit_smax_ = ORD ? SMAX : jit_default_smax(MW, SMAX);
     if (ORD) cfg_.jit = 1;  // no run-time specialisation of the ordered kernel
+    if (ORD && cfg_.tiebreak)
+      throw Error(QI_ERR_UNSUPPORTED,
+                  "QI_TIE_RANDOM: the order-exact kernel (threshold-0 quorum sets, SCCs beyond 256 vertices) only has "
+                  "the lowest-index rule");
     stream_ = acquire_stream(device_);
     HIP_CHECK(hipEventCreate(&e0_));
     HIP_CHECK(hipEventCreate(&e1_));
@@ -893,6 +897,8 @@ class SearchDeviceImpl : public SearchDevice {
     a.best64 = best64_;
     a.xbest = xbest_dev_ ? xbest_dev_ : best64_;
     a.poll_rep = poll_rep_;
+    a.tiebreak = cfg_.tiebreak;
+    a.tie_seed = cfg_.tie_seed;
     a.grow_budget = cfg_.grow_budget;
     a.run_budget = cfg_.run_budget;
     a.grace = cfg_.grace;

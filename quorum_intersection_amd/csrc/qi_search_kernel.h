@@ -196,6 +196,80 @@ __device__ __forceinline__ uint32_t best_node(const LocalDev& f, const uint32_t 
   return bestv;
 }
 
+// findBestNode with the reference's own rule (cpp:229-246): uniform over the vertices of
+// Q \ D with the maximal in-degree.  The reference draws from a process-global random
+// engine; here the draw is a hash of (seed, path key, depth) of the node, so a search is
+// reproducible and independent of the schedule.  `pick` = that hash.
+template <int MW>
+__device__ __noinline__ uint32_t best_node_random(const LocalDev& f, const uint32_t (&Q)[MW], const uint32_t (&D)[MW],
+                                                  uint32_t& zero_fallback, uint32_t pick) {
+  uint32_t bestdeg = 0;
+  uint32_t C[MW];  // candidates with the best degree so far
+#pragma unroll
+  for (int w = 0; w < MW; ++w) C[w] = 0u;
+  bool any = false;
+  for (uint32_t g = 0; g < f.G; ++g) {
+    uint32_t deg = 0, cand_any = 0;
+    uint32_t M[MW];
+#pragma unroll
+    for (int w = 0; w < MW; ++w) {
+      deg += __popc(Q[w] & K(f.grp_col)[g * MW + w]);
+      M[w] = Q[w] & ~D[w] & K(f.grp_members)[g * MW + w];
+      cand_any |= M[w];
+    }
+    const uint32_t e0 = K(f.grp_extra_off)[g], e1 = K(f.grp_extra_off)[g + 1];
+    for (uint32_t e = e0; e < e1; ++e) {
+#pragma unroll
+      for (int w = 0; w < MW; ++w) deg += __popc(Q[w] & K(f.grp_extra)[e * MW + w]);
+    }
+    if (!cand_any) continue;
+    if (!any || deg > bestdeg) {
+      any = true;
+      bestdeg = deg;
+#pragma unroll
+      for (int w = 0; w < MW; ++w) C[w] = M[w];
+    } else if (deg == bestdeg) {
+#pragma unroll
+      for (int w = 0; w < MW; ++w) C[w] |= M[w];
+    }
+  }
+  zero_fallback += (bestdeg == 0u) ? 1u : 0u;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int w = 0; w < MW; ++w) cnt += __popc(C[w]);
+  if (!cnt) return 0xFFFFFFFFu;
+  uint32_t k = pick % cnt;
+  uint32_t v = 0xFFFFFFFFu;
+#pragma unroll
+  for (int w = 0; w < MW; ++w) {
+    const uint32_t c = __popc(C[w]);
+    if (v == 0xFFFFFFFFu) {
+      if (k < c) {
+        uint32_t x = C[w];
+        for (uint32_t i = 0; i < k; ++i) x &= x - 1u;  // drop the k lowest candidates
+        v = (uint32_t)w * 32u + (uint32_t)__builtin_ctz(x);
+      } else {
+        k -= c;
+      }
+    }
+  }
+  return v;
+}
+
+// The draw of a node: a mix of the seed, its path key and its depth.
+template <int MW>
+__device__ __forceinline__ uint32_t tie_hash(uint32_t seed, const uint32_t (&Kk)[MW], uint32_t depth) {
+  uint32_t h = seed ^ (depth * 0x9E3779B9u);
+#pragma unroll
+  for (int w = 0; w < MW; ++w) {
+    h ^= Kk[w] + 0x7F4A7C15u + (h << 6) + (h >> 2);
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+  }
+  h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
+
 // The generic evaluator: interprets the packed TN table (any FBAS shape).  A runtime-
 // specialised evaluator with the same interface is generated per FBAS (qi_jit.cpp).
 template <int MW, int TW>
@@ -319,6 +393,8 @@ struct SearchArgs {
                                  // wave polling ONE best key / queue head serialised at that line
                                  // (~25 ns per access: 0.8 ms per search at 64-iteration polls).
   uint32_t seq;                  // this launch's sequence number (unique per engine, never 0xFFFFFFFF)
+  uint32_t tiebreak;             // findBestNode ties: 0 lowest vertex index, 1 the seeded uniform draw
+  uint32_t tie_seed;
   uint32_t grow_budget;          // per-lane node budget while the frontier is below half the lanes
   uint32_t run_budget;
   uint32_t grace;                // extra steps per lane once the unit queue is dry
@@ -942,7 +1018,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           if (!qne || dout || !qd) {  // cpp:303, 308-314, 325
             has = false;
           } else {
-            const uint32_t pb = EV::best(f, X, D, seg_zfb);  // cpp:317
+            const uint32_t pb = a.tiebreak ? best_node_random<MW>(f, X, D, seg_zfb, tie_hash<MW>(a.tie_seed, K, depth))
+                                           : EV::best(f, X, D, seg_zfb);  // cpp:317
 #pragma unroll
             for (int w = 0; w < MW; ++w) X[w] &= ~D[w];
             X[pb >> 5] &= ~(1u << (pb & 31u));  // toRemove' = Q \ D \ {b} (cpp:330-334)
@@ -1163,7 +1240,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (!qne || dout || !qd) {  // cpp:303, 308-314, 325
         has = false;
       } else {
-        pb = EV::best(f, X, D, seg_zfb);  // cpp:317
+        pb = a.tiebreak ? best_node_random<MW>(f, X, D, seg_zfb, tie_hash<MW>(a.tie_seed, K, depth))
+                        : EV::best(f, X, D, seg_zfb);  // cpp:317
 #pragma unroll
         for (int w = 0; w < MW; ++w) X[w] &= ~D[w];
         X[pb >> 5] &= ~(1u << (pb & 31u));  // toRemove' = Q \ D \ {b} (cpp:330-334)

@@ -291,6 +291,44 @@ def test_multiword_random_exact():
         _cmp(qa.FBAS(text).solve_stats(), r, f"big{seed}")
 
 
+# ---- the reference's own tie-break: uniform over the maximal in-degree vertices ------------
+@pytest.mark.parametrize("jit", [1, 2], ids=["table", "specialised"])
+def test_random_tiebreak_verdicts_match_oracle(jit):
+    # cpp:229-246 draws uniformly among the argmax vertices; QI_TIE_RANDOM does the same with
+    # a seeded draw per node.  Verdicts are invariant under the rule: they must equal the
+    # oracle's TIE_RANDOM (and TIE_LOWEST) verdicts on the fixtures and on random FBAS; the
+    # witness of a "false" is validated independently; node counts may differ.
+    cases = [(n, fixture_text(n)) for n in FIXTURES]
+    cases += [(f"org{seed}", random_org_fbas(seed, n_orgs=5 + seed % 4)) for seed in range(20)]
+    cases += [("tiered_5", fbas_gen.tiered(5)), ("planted_5_96", fbas_gen.planted(5, 96))]
+    differing = 0
+    for name, text in cases:
+        g = Oracle().load(text)
+        want = g.solve(tiebreak=1, seed=7)
+        low = qa.FBAS(text).solve_stats(jit=jit)
+        for seed in (1, 2):
+            d = qa.FBAS(text).solve_stats(jit=jit, tiebreak=1, tie_seed=seed)
+            assert d["verdict"] == want["verdict"] == low["verdict"], (name, seed)
+            assert d["searched"] == want["searched"]
+            if d["searched"] and not d["verdict"]:
+                _validate_witness(text, d["q1"], d["q2"])
+            differing += d["nodes"] != low["nodes"]
+    assert differing > 0  # the draws do change the tree somewhere
+
+
+def test_random_tiebreak_is_reproducible_and_sharded():
+    text = fbas_gen.tiered(6)
+    a = qa.FBAS(text).solve_stats(jit=2, tiebreak=1, tie_seed=5)
+    b = qa.FBAS(text).solve_stats(jit=1, tiebreak=1, tie_seed=5)
+    c = qa.FBAS(text).solve_stats(jit=2, tiebreak=1, tie_seed=5, engines=3, device_mask=1)
+    key = ("verdict", "nodes", "evals", "minq")
+    assert [a[k] for k in key] == [b[k] for k in key] == [c[k] for k in key]
+    assert a["verdict"] is True
+    with pytest.raises(qa.QIError) as e:  # the order-exact kernel has the lowest-index rule only
+        qa.FBAS(_text_for("random_28")).solve_stats(tiebreak=1)
+    assert e.value.code == 4
+
+
 # ---- text outputs (-v / -g) ------------------------------------------------------------
 @pytest.mark.parametrize("name", FIXTURES)
 def test_solve_text_matches_oracle(name):
