@@ -148,6 +148,7 @@ SIGNATURES = {
 }
 
 _lib = None
+torch_first = True  # False once the library was loaded in a process that had not imported torch
 
 
 def lib() -> ctypes.CDLL:
@@ -158,13 +159,20 @@ def lib() -> ctypes.CDLL:
             raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc, gfx950) first")
         # PyTorch-ROCm ships its own libamdhip64.so.7 (ROCm 7.0) with the same soname as
         # /opt/rocm's (7.2): whichever loads first serves the whole process, and torch
-        # then refuses a runtime that is not its own ("No HIP GPUs are available").  Load
-        # torch's first, so the kernels and torch tensors/RCCL (multi-rank hand-offs)
-        # share one HIP runtime.  Without torch the system runtime is used.
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # then refuses a runtime that is not its own ("No HIP GPUs are available").  A
+        # process that uses torch beside this library (the multi-rank driver, tests moving
+        # units through tensors) must therefore load torch FIRST: import torch before the
+        # first call into this package, or set QI_TORCH_RUNTIME=1 and it is imported here.
+        # Otherwise torch is not touched (no seconds of import, and the system runtime the
+        # library was built against is used).
+        import sys
+        if os.environ.get("QI_TORCH_RUNTIME") == "1" and "torch" not in sys.modules:
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
+        global torch_first
+        torch_first = "torch" in sys.modules
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

@@ -64,9 +64,10 @@ namespace qi {
 namespace dev {
 
 // Ahead-of-time kernels: one per (vertex words, TN words, stack depth) shape.
-template <int MW, int TW, int SMAX>
+// (TIE: findBestNode's tie rule, see search_body)
+template <int MW, int TW, int SMAX, bool TIE>
 __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
-  search_body<MW, TW, SMAX, TableEval<MW, TW>>(a);
+  search_body<MW, TW, SMAX, TableEval<MW, TW>, TIE>(a);
 }
 
 // Order-exact search for SCCs with threshold-0 quorum sets (qi_ordered_kernel.h).
@@ -772,7 +773,7 @@ class SearchDeviceImpl : public SearchDevice {
       // auto / cache-only: a specialised kernel already in the on-disk cache runs from the
       // first launch (hipModuleLoadData, ~1 ms); auto compiles a missing one in the
       // background once the search proves long (step()), cache-only never compiles
-      jit_code_ = jit_cached(jit_source(flat_, MW, TW, jit_smax_, false));
+      jit_code_ = jit_cached(jit_source(flat_, MW, TW, jit_smax_, false, cfg_.tiebreak != 0));
       if (!jit_code_.empty()) {
         jit_state_.store(2);
         load_jit();
@@ -941,7 +942,8 @@ class SearchDeviceImpl : public SearchDevice {
         void* args[] = {&a};
         HIP_CHECK(hipModuleLaunchKernel(jit_fn_, blocks, 1, 1, 64, 1, 1, (unsigned)jit_shm_, stream_, args, nullptr));
       } else {
-        hipLaunchKernelGGL((dev::search_kernel<MW, TW, SMAX>), dim3(blocks), dim3(64), shm_, stream_, a);
+        if (cfg_.tiebreak) hipLaunchKernelGGL((dev::search_kernel<MW, TW, SMAX, true>), dim3(blocks), dim3(64), shm_, stream_, a);
+        else hipLaunchKernelGGL((dev::search_kernel<MW, TW, SMAX, false>), dim3(blocks), dim3(64), shm_, stream_, a);
       }
       HIP_CHECK(hipGetLastError());
       if (trace_) HIP_CHECK(hipEventRecord(ev_[k + 1], stream_));  // per-launch times: diagnostics only
@@ -1034,9 +1036,20 @@ class SearchDeviceImpl : public SearchDevice {
         HIP_CHECK(hipEventElapsedTime(&ms, ev_[k], ev_[k + 1]));
         ms_sum += ms;
       }
-      if (trace_)
-        std::fprintf(stderr, "[qi]     launch %u: in %u out %u halt %u, %.1f us\n", k, c[dev::HC_NIN], c[dev::HC_OUT],
+      if (trace_) {
+        std::fprintf(stderr, "[qi]     launch %u: in %u out %u halt %u, %.1f us", k, c[dev::HC_NIN], c[dev::HC_OUT],
                      c[dev::HC_HALT], ms * 1e3);
+        if (c[dev::HC_DIAG + 1])  // a QI_DIAG_LAUNCH build: this launch's nodes and wave iterations
+          std::fprintf(stderr, ", nodes %u wave-iters %u", c[dev::HC_DIAG] - (c[dev::HC_DIAG] >= diag_prev_[0] ? diag_prev_[0] : 0u),
+                       c[dev::HC_DIAG + 1] - (c[dev::HC_DIAG + 1] >= diag_prev_[1] ? diag_prev_[1] : 0u));
+        if (c[dev::HC_DIAG + 1])
+          std::fprintf(stderr, " (max %u), wave us avg %.1f max %.1f span %.1f", c[dev::HC_DIAG + 2],
+                       c[dev::HC_DIAG + 3] * 0.01 / std::max(1u, std::min((c[dev::HC_NIN] + 63u) / 64u, blocks)),
+                       c[dev::HC_DIAG + 4] * 0.01, c[dev::HC_DIAG + 5] * 0.01);
+        diag_prev_[0] = c[dev::HC_DIAG];
+        diag_prev_[1] = c[dev::HC_DIAG + 1];
+        std::fprintf(stderr, "\n");
+      }
     }
     if (!trace_) ms_sum = si.dispatch_ms;  // the chain's kernels back to back (<= 2 empty launches at its end)
     n_ = n_next;
@@ -1428,6 +1441,7 @@ class SearchDeviceImpl : public SearchDevice {
   uint32_t best_depth_ = 0;
   bool best_dirty_ = false;
   bool trace_ = false;
+  uint32_t diag_prev_[2] = {0, 0};
   bool has_local_best_ = false;
   Witness local_best_;
   double sum_ms_ = 0;
@@ -1446,7 +1460,7 @@ class SearchDeviceImpl : public SearchDevice {
 
   void start_jit() {
     jit_state_.store(1);
-    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3);
+    std::string src = jit_source(flat_, MW, TW, jit_smax_, cfg_.jit == 3, cfg_.tiebreak != 0);
     jit_thread_ = std::thread([this, src]() {
       std::vector<char> code = jit_compile(src, &jit_log_);
       jit_code_ = std::move(code);
@@ -1462,7 +1476,7 @@ class SearchDeviceImpl : public SearchDevice {
     DeviceGuard dg(device_);
     const void* kfn;
     if constexpr (ORD) kfn = (const void*)dev::ordered_kernel<MW, TW>;
-    else kfn = (const void*)dev::search_kernel<MW, TW, SMAX>;
+    else kfn = cfg_.tiebreak ? (const void*)dev::search_kernel<MW, TW, SMAX, true> : (const void*)dev::search_kernel<MW, TW, SMAX, false>;
     if (!ORD) HIP_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_));
     if (!cfg_.max_blocks) {  // one resident wave of blocks: no second-wave tail
       int nb = 0;

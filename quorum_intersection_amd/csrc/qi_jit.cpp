@@ -199,7 +199,7 @@ std::vector<SlicedGroup> find_sliced_groups(const LocalFlat& f, std::vector<int>
 
 }  // namespace
 
-std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps) {
+std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps, bool tie_random) {
   std::ostringstream o;
   if (stamps) o << "#define QI_STAMPS 1\n";
   o << "#define QI_LDS_OW " << jit_lds_ow(f) << "\n";  // D-order words per lane: |D| <= m/2 + 1
@@ -507,7 +507,8 @@ std::string jit_source(const LocalFlat& f, int MW, int TW, int SMAX, bool stamps
   o << "  static __device__ __forceinline__ uint32_t qmin0(const LocalDev&) { return " << f.qmin[0] << "u; }\n};\n";
   o << "}  // namespace dev\n}  // namespace qi\n\n";
   o << "extern \"C\" __global__ __launch_bounds__(64) void qi_search_spec(qi::dev::SearchArgs a) {\n"
-    << "  qi::dev::search_body<" << MW << ", " << TW << ", " << SMAX << ", qi::dev::SpecEval>(a);\n}\n";
+    << "  qi::dev::search_body<" << MW << ", " << TW << ", " << SMAX << ", qi::dev::SpecEval, " << (tie_random ? "true" : "false")
+    << ">(a);\n}\n";
   return o.str();
 }
 

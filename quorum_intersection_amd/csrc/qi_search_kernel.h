@@ -201,7 +201,7 @@ __device__ __forceinline__ uint32_t best_node(const LocalDev& f, const uint32_t 
 // engine; here the draw is a hash of (seed, path key, depth) of the node, so a search is
 // reproducible and independent of the schedule.  `pick` = that hash.
 template <int MW>
-__device__ __noinline__ uint32_t best_node_random(const LocalDev& f, const uint32_t (&Q)[MW], const uint32_t (&D)[MW],
+__device__ __forceinline__ uint32_t best_node_random(const LocalDev& f, const uint32_t (&Q)[MW], const uint32_t (&D)[MW],
                                                   uint32_t& zero_fallback, uint32_t pick) {
   uint32_t bestdeg = 0;
   uint32_t C[MW];  // candidates with the best degree so far
@@ -324,32 +324,43 @@ struct WitLayout {
 // Per-launch counter block (CTR_WORDS words).  Launches are chained on the device: launch
 // k reads its input count, log position and stop state from launch k-1's block (or from a
 // host-written seed block), so the host enqueues launches without reading anything back
-// in between.  The atomically updated words and the plainly written ones sit on separate
-// 128-B lines.  The last block of a launch carries never-claimed input units over and
-// publishes the final block to pinned host memory (HC_* words), where the host polls it.
+// in between.  Every atomically updated word has a 128-B line of its own: atomics of many
+// waves on one line are served one at a time (measured 11.5 ns each, returned or not, same
+// word or not: tools/atomic_probe.hip), so a full grid's claims, spill reservations and
+// finish counts on ONE line put a floor of ~130 us under a launch whose waves end together.
+// The last block of a launch carries never-claimed input units over and publishes the
+// final block to pinned host memory (HC_* words), where the host polls it.
 enum : int {
   C_OUT = 0,       // units written to units_out (spills + carried-over units)   [atomic]
-  C_HEAD = 1,      // dynamic claims past the statically assigned range           [atomic]
-  C_DONE = 2,      // used blocks that finished                                   [atomic]
-  C_EVX = 4,       // stack evictions granted from the shared output pool          [atomic]
-  C_NIN = 32,      // input units of this launch (the previous block's C_OUT)
-  C_LOGB = 33,     // first segment-log record of this launch
-  C_STOP = 34,     // 1: capacity would be exceeded; this launch (and the rest of the chain) did nothing
-  C_STATIC = 35,   // end of the statically assigned range (64 units per used block)
-  C_LOGN = 36,     // log base of the next launch (written by this launch's last block)
-  C_HALT = 37,     // 1: this launch carried units over (its lanes ran out of budget with
+#ifdef QI_CTR_PACKED  // diagnostics: the four atomic words on one line
+  C_HEAD = 1, C_DONE = 2, C_EVX = 4,
+#else
+  C_HEAD = 32,     // dynamic claims past the statically assigned range           [atomic]
+  C_DONE = 64,     // used blocks that finished                                   [atomic]
+  C_EVX = 96,      // stack evictions granted from the shared output pool          [atomic]
+#endif
+  C_DIAG = 100,    // QI_DIAG_LAUNCH: max wave iterations, sum / max wave ticks, max ~start, max end [atomic]
+  C_NIN = 128,     // input units of this launch (the previous block's C_OUT)
+  C_LOGB = 129,    // first segment-log record of this launch
+  C_STOP = 130,    // 1: capacity would be exceeded; this launch (and the rest of the chain) did nothing
+  C_STATIC = 131,  // end of the statically assigned range (64 units per used block)
+  C_LOGN = 132,    // log base of the next launch (written by this launch's last block)
+  C_HALT = 133,    // 1: this launch carried units over (its lanes ran out of budget with
                    // units left); the rest of the chain does nothing and the host sorts
                    // the frontier into preorder before it goes on
-  C_PEAKED = 38,   // launches of the chain so far that ran with the run budget (> 0: the
+  C_PEAKED = 134,  // launches of the chain so far that ran with the run budget (> 0: the
                    // frontier has covered the lanes once, what follows is its decay)
-  CTR_WORDS = 64,
+  CTR_WORDS = 160,
   HC_OUT = 0, HC_NIN = 1, HC_LOGB = 2, HC_STOP = 3, HC_DONE = 4, HC_LOGN = 5, HC_HALT = 6,
   HC_BEST = 8,     // u64 (two words): the device-side best key after this launch
   HC_FLAG = 10,    // u64, ONE 8-byte store, written last: bit 63 = published, bit 62 = stopped,
                    // low 32 bits = units out.  The host spins on it in pinned memory to pace
                    // its look-ahead (no event per launch); the other words are read after
                    // the chain's final stream synchronisation.
-  HC_WORDS = 16
+  HC_DIAG = 16,    // kernels built with QI_DIAG_LAUNCH only: running nodes, running wave iterations, then
+                   // of this launch: max wave iterations, sum and max of the waves' run times and the
+                   // span first wave start .. last wave end (10 ns ticks)
+  HC_WORDS = 32
 };
 // Output capacity per launch: n_in (carried-over units) + per used lane SPILL_RESERVE(S)
 // units for its one final spill (current node, top of stack, S stacked entries, a claimed
@@ -394,6 +405,7 @@ struct SearchArgs {
                                  // (~25 ns per access: 0.8 ms per search at 64-iteration polls).
   uint32_t seq;                  // this launch's sequence number (unique per engine, never 0xFFFFFFFF)
   uint32_t tiebreak;             // findBestNode ties: 0 lowest vertex index, 1 the seeded uniform draw
+                                 // (informational: the rule is compiled into the kernel, search_body's TIE)
   uint32_t tie_seed;
   uint32_t grow_budget;          // per-lane node budget while the frontier is below half the lanes
   uint32_t run_budget;
@@ -597,7 +609,9 @@ constexpr int stamp_bucket(int f) {
 #define QI_FLUSH_AFTER 1
 #endif
 
-template <int MW, int TW, int SMAX, class EV>
+// TIE: findBestNode's tie rule, fixed per kernel (a run-time choice in the node loop cost
+// 15-50 % per search): false = lowest vertex index, true = the seeded uniform draw.
+template <int MW, int TW, int SMAX, class EV, bool TIE = false>
 __device__ __forceinline__ void search_body(const SearchArgs& a) {
   using UL = UnitLayout<MW>;
   using RL = RecLayout<MW>;
@@ -702,6 +716,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   bool must_spill = false;  // an eviction found the pool empty: spill at the next iteration
   uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
   bool dry = false;         // wave-uniform: no unit left to claim (head >= n_in)
+  // wave-uniform: the iteration at which a dry wave spills whatever its lanes still hold --
+  // all lanes at once, so the wave reserves its output slots with ONE atomic
+  uint32_t force_at = 0xFFFFFFFFu;
   uint32_t iter = 0;        // wave-uniform: iterations so far, fast steps included
   uint32_t next_poll = 0;   // the poll is due in the first full iteration with iter >= next_poll
   bool poll_issued = true;  // its loads are in flight (the first ones are issued before the loop)
@@ -726,6 +743,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint64_t stamp_sum[6] = {0, 0, 0, 0, 0, 0};
   uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
   const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef QI_DIAG_LAUNCH
+  const uint32_t diag_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
   uint64_t best64 = ~0ull;
   // lane 0's poll loads are issued one iteration before the poll that reads them, so
@@ -939,6 +959,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
       dry = true;
       limit = min(limit, steps + a.grace);
+      force_at = wave_iters + a.grace;
     }
   };
 
@@ -1018,8 +1039,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           if (!qne || dout || !qd) {  // cpp:303, 308-314, 325
             has = false;
           } else {
-            const uint32_t pb = a.tiebreak ? best_node_random<MW>(f, X, D, seg_zfb, tie_hash<MW>(a.tie_seed, K, depth))
-                                           : EV::best(f, X, D, seg_zfb);  // cpp:317
+            uint32_t pb;  // cpp:317
+            if constexpr (TIE) pb = best_node_random<MW>(f, X, D, seg_zfb, tie_hash<MW>(a.tie_seed, K, depth));
+            else pb = EV::best(f, X, D, seg_zfb);
 #pragma unroll
             for (int w = 0; w < MW; ++w) X[w] &= ~D[w];
             X[pb >> 5] &= ~(1u << (pb & 31u));  // toRemove' = Q \ D \ {b} (cpp:330-334)
@@ -1048,6 +1070,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
     QI_STAMP(F_FAST);
+#endif
+    // the grace period of a dry wave is over: every lane spills in this iteration (per-lane
+    // step limits alone would let lanes that idled during the grace period lag behind)
+#ifndef QI_NO_FORCE_SPILL
+    if (wave_iters >= force_at) limit = 0;
 #endif
     // ---- (1) lanes without a node: pop the top of stack, else install the next unit ----
     if (!done && !has) {
@@ -1165,6 +1192,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (dry_poll && !dry && d == a.seq) {
         dry = true;
         limit = min(limit, steps + a.grace);
+        force_at = wave_iters + a.grace;
       }
     } else if (!poll_issued && iter + 2u * ((uint32_t)QI_FAST_STEPS + 1u) >= next_poll) {
       // at least one full iteration before the poll that reads them
@@ -1172,7 +1200,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (lane == 0) issue_poll();
     }
     ++iter;
-
     QI_STAMP(F_POLL);
     // ---- (3) budget exhausted: spill current node, top, stack and claimed unit ---------
     {
@@ -1240,8 +1267,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (!qne || dout || !qd) {  // cpp:303, 308-314, 325
         has = false;
       } else {
-        pb = a.tiebreak ? best_node_random<MW>(f, X, D, seg_zfb, tie_hash<MW>(a.tie_seed, K, depth))
-                        : EV::best(f, X, D, seg_zfb);  // cpp:317
+        if constexpr (TIE) pb = best_node_random<MW>(f, X, D, seg_zfb, tie_hash<MW>(a.tie_seed, K, depth));
+        else pb = EV::best(f, X, D, seg_zfb);  // cpp:317
 #pragma unroll
         for (int w = 0; w < MW; ++w) X[w] &= ~D[w];
         X[pb >> 5] &= ~(1u << (pb & 31u));  // toRemove' = Q \ D \ {b} (cpp:330-334)
@@ -1538,6 +1565,16 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #endif
   }
 
+#ifdef QI_DIAG_LAUNCH
+  if (lane == 0) {
+    const uint32_t t1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    atomicMax(&cc[C_DIAG], wave_iters);
+    atomicAdd(&cc[C_DIAG + 1], t1 - diag_t0);
+    atomicMax(&cc[C_DIAG + 2], t1 - diag_t0);
+    atomicMax(&cc[C_DIAG + 3], ~diag_t0);
+    atomicMax(&cc[C_DIAG + 4], t1);
+  }
+#endif
   // ---- last block of the launch: carry over never-claimed input units (whose waves all
   // hit their budget before the queue ran dry) with zeroed records, publish the counters.
   // Every counter read here is an atomic RMW, performed after the other blocks' returned
@@ -1556,6 +1593,25 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         a.host_ctr[HC_BEST] = (uint32_t)bb;
         a.host_ctr[HC_BEST + 1] = (uint32_t)(bb >> 32);
       }
+#ifdef QI_DIAG_LAUNCH  // diagnostics: running node / wave-iteration totals after this launch (low words)
+      {
+        unsigned long long dn = atomicAdd(&a.totals[(size_t)lane * 16 + 0], 0ull);
+        unsigned long long di = atomicAdd(&a.totals[(size_t)lane * 16 + 6], 0ull);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          dn += __shfl_xor(dn, d);
+          di += __shfl_xor(di, d);
+        }
+        if (lane == 0) {
+          a.host_ctr[HC_DIAG] = (uint32_t)dn;
+          a.host_ctr[HC_DIAG + 1] = (uint32_t)di;
+          a.host_ctr[HC_DIAG + 2] = atomicAdd(&cc[C_DIAG], 0u);
+          a.host_ctr[HC_DIAG + 3] = atomicAdd(&cc[C_DIAG + 1], 0u);
+          a.host_ctr[HC_DIAG + 4] = atomicAdd(&cc[C_DIAG + 2], 0u);
+          a.host_ctr[HC_DIAG + 5] = atomicAdd(&cc[C_DIAG + 4], 0u) + atomicAdd(&cc[C_DIAG + 3], 0u) + 1u;  // end - start
+        }
+      }
+#endif
       hd = lane0(hd);
       out = lane0(out);
       const uint32_t lane0_out = out;

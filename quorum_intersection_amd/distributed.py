@@ -35,6 +35,13 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from . import _capi
+
+if not _capi.torch_first:
+    raise ImportError("quorum_intersection_amd.distributed: the HIP library was loaded before torch, so the process "
+                      "runs on another HIP runtime than torch's; import torch (or this module) before the first "
+                      "call into the package, or set QI_TORCH_RUNTIME=1")
+
 Key = Tuple[Tuple[int, ...], int]  # (path key words, depth); preorder = lexicographic
 
 

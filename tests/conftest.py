@@ -3,6 +3,9 @@ import sys
 
 import pytest
 
+# the GPU tests move frontier units through torch tensors: torch's HIP runtime must be the
+# process's (quorum_intersection_amd._capi.lib)
+os.environ.setdefault("QI_TORCH_RUNTIME", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -158,7 +158,8 @@ def random_org_fbas(seed: int, n_orgs: int = 6, quirks: bool = True, t0: bool = 
     """Search-heavy random FBAS: organisations of 1-4 validators whose quorum sets are
     random threshold trees over organisations (so the main SCC is large), with
     occasional duplicate refs, outside/unknown refs and t > entries; threshold 0 only
-    with t0=True (anti-monotone slices: search parity is unpinned there)."""
+    with t0=True (anti-monotone slices: the search then runs the order-exact kernel, whose
+    counts and witnesses are compared with the oracle like any other)."""
     rng = random.Random(seed)
     orgs = []
     for o in range(n_orgs):
