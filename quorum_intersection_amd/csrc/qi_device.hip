@@ -1046,6 +1046,12 @@ class SearchDeviceImpl : public SearchDevice {
           std::fprintf(stderr, " (max %u), wave us avg %.1f max %.1f span %.1f", c[dev::HC_DIAG + 2],
                        c[dev::HC_DIAG + 3] * 0.01 / std::max(1u, std::min((c[dev::HC_NIN] + 63u) / 64u, blocks)),
                        c[dev::HC_DIAG + 4] * 0.01, c[dev::HC_DIAG + 5] * 0.01);
+        if (c[dev::HC_DIAG + 6]) {  // waves that went dry and spilled: average phase times
+          const double w = 0.01 / c[dev::HC_DIAG + 6];
+          std::fprintf(stderr, "; %u dry waves: start %.1f, to dry %.1f, grace %.1f, spill %.1f (slot wait %.1f), end %.1f us",
+                       c[dev::HC_DIAG + 6], c[dev::HC_DIAG + 7] * w, c[dev::HC_DIAG + 8] * w, c[dev::HC_DIAG + 9] * w,
+                       c[dev::HC_DIAG + 10] * w, c[dev::HC_DIAG + 12] * w, c[dev::HC_DIAG + 11] * w);
+        }
         diag_prev_[0] = c[dev::HC_DIAG];
         diag_prev_[1] = c[dev::HC_DIAG + 1];
         std::fprintf(stderr, "\n");

@@ -601,6 +601,11 @@ constexpr int stamp_bucket(int f) {
 #ifndef QI_DECAY_RUN
 #define QI_DECAY_RUN 2
 #endif
+// fast steps of a dry wave run with this many eligible lanes (no unit can be installed any
+// more, so waiting for a full iteration serves only quorum leaves and full stacks)
+#ifndef QI_FAST_MIN_DRY
+#define QI_FAST_MIN_DRY 8
+#endif
 // claim the next units (and flush records) right after the installs instead of after the push
 #ifndef QI_CLAIM_FIRST
 #define QI_CLAIM_FIRST 0
@@ -629,6 +634,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // loaded when installed
   constexpr bool PREFETCH = UW <= 20;
   constexpr int FW = PREFETCH ? UW : 4;
+#ifdef QI_WORD_STORES  // diagnostics: units and records leave word by word
+  constexpr bool WIDE = false;
+#else
+  constexpr bool WIDE = PREFETCH;
+#endif
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* st = lds;                                          // [SMAX][SE][64]
   uint32_t* co_NE = st + SMAX * SE * WAVE;                      // [MW][64] per pending rank
@@ -746,6 +756,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #endif
 #ifdef QI_DIAG_LAUNCH
   const uint32_t diag_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  uint32_t diag_dry = 0, diag_sp0 = 0, diag_spr = 0, diag_sp1 = 0, diag_loop0 = 0;  // 0 = did not happen
+#define QI_DIAG_MARK(v) do { if (!(v)) (v) = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u; } while (0)
+#else
+#define QI_DIAG_MARK(v) do { } while (0)
 #endif
   uint64_t best64 = ~0ull;
   // lane 0's poll loads are issued one iteration before the poll that reads them, so
@@ -804,8 +818,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     if (rec_pend) {
 #ifndef QI_ABL_NOREC  // diagnostics: no record stores (counts then only via the running totals)
       uint32_t* r = records + (size_t)rec_idx * RL::WORDS;
+      if constexpr (WIDE && RL::WORDS % 2 == 0) {  // 8-byte stores (record stride and log base are 8-byte multiples)
 #pragma unroll
-      for (int w = 0; w < RL::WORDS; ++w) r[w] = rec[w];
+        for (int w = 0; w < RL::WORDS; w += 2) *(uint2*)(r + w) = make_uint2(rec[w], rec[w + 1]);
+      } else {
+#pragma unroll
+        for (int w = 0; w < RL::WORDS; ++w) r[w] = rec[w];
+      }
 #endif
       rec_pend = false;
     }
@@ -844,13 +863,42 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       return;
     }
     uint32_t* u = a.units_out + (size_t)slot * UW;
+    const uint32_t ulen = ol + (extra_b >= 0 ? 1u : 0u);
+    if constexpr (WIDE) {
+      // small units go out whole, as 16-byte stores: a launch end writes ~4 units per lane,
+      // and word-by-word (4-byte stores 48 B apart across the wave) that took 50-90 us of a
+      // decaying launch's ~300
+      uint32_t uw[UW];
+#pragma unroll
+      for (int q = 0; q < UW; ++q) uw[q] = 0u;
+#pragma unroll
+      for (int w = 0; w < MW; ++w) {
+        uw[UL::T_ + w] = UT[w];
+        uw[UL::D_ + w] = UD[w];
+        uw[UL::K_ + w] = UK[w];
+      }
+      uw[UL::DEPTH] = udepth;
+      uw[UL::DLEN] = ulen;
+#pragma unroll
+      for (int i = 0; i < OW && UL::ORD + i < UW; ++i) {  // bytes >= ulen are don't-care
+        uint32_t word = DOW_(i);
+        if (extra_b >= 0 && (uint32_t)i == (ol >> 2)) {
+          const uint32_t sh = 8u * (ol & 3u);
+          word = (word & ~(0xFFu << sh)) | ((uint32_t)extra_b << sh);
+        }
+        uw[UL::ORD + i] = word;
+      }
+      uint4* u4 = (uint4*)u;
+#pragma unroll
+      for (int q = 0; q < UW / 4; ++q) u4[q] = make_uint4(uw[4 * q], uw[4 * q + 1], uw[4 * q + 2], uw[4 * q + 3]);
+      return;
+    }
 #pragma unroll
     for (int w = 0; w < MW; ++w) {
       u[UL::T_ + w] = UT[w];
       u[UL::D_ + w] = UD[w];
       u[UL::K_ + w] = UK[w];
     }
-    const uint32_t ulen = ol + (extra_b >= 0 ? 1u : 0u);
     u[UL::DEPTH] = udepth;
     u[UL::DLEN] = ulen;
     for (uint32_t i = 0; i < (ulen + 3) / 4; ++i) {  // bytes >= ulen are don't-care
@@ -883,15 +931,26 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // a claimed but not installed unit goes back out unchanged, its record zeroed
   auto write_claimed = [&](uint32_t slot) {
     uint32_t* r = records + (size_t)fidx * RL::WORDS;
+    if constexpr (WIDE && RL::WORDS % 2 == 0) {
 #pragma unroll
-    for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
+      for (int w = 0; w < RL::WORDS; w += 2) *(uint2*)(r + w) = make_uint2(0u, 0u);
+    } else {
+#pragma unroll
+      for (int w = 0; w < RL::WORDS; ++w) r[w] = 0u;
+    }
     if (slot >= a.out_cap) {
       atomicOr(&a.glob[1], FLAG_OUT_OVERFLOW);
       return;
     }
     uint32_t* u = a.units_out + (size_t)slot * UW;
+    if constexpr (WIDE) {
+      uint4* u4 = (uint4*)u;
 #pragma unroll
-    for (int q = 0; q < UW; ++q) u[q] = unit_word(q);
+      for (int q = 0; q < UW / 4; ++q) u4[q] = make_uint4(fdat[4 * q], fdat[4 * q + 1], fdat[4 * q + 2], fdat[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < UW; ++q) u[q] = unit_word(q);
+    }
   };
 
   // D is a minimal quorum (cpp:283-285): credit cpp:184, |D| x cpp:192 and the visitor
@@ -958,12 +1017,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     }
     if (pool_dead && !dry) {  // the queue ran out: grace period, then spill
       dry = true;
+      QI_DIAG_MARK(diag_dry);
       limit = min(limit, steps + a.grace);
       force_at = wave_iters + a.grace;
     }
   };
 
   for (;;) {
+    QI_DIAG_MARK(diag_loop0);
 #if QI_FAST_STEPS > 0
     // ---- (0) fast steps: pop or process one node per lane, common outcomes only --------
     // A lane whose node is a quorum leaf (cpp:281) or whose push would need an eviction is
@@ -974,7 +1035,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll 1
       for (int fs = 0; fs < QI_FAST_STEPS; ++fs) {
         const bool elig = !done && !hold && (has || tvalid);
-        if ((uint32_t)__popcll(__ballot(elig)) < (uint32_t)QI_FAST_MIN) break;
+        if ((uint32_t)__popcll(__ballot(elig)) < (dry ? (uint32_t)QI_FAST_MIN_DRY : (uint32_t)QI_FAST_MIN)) break;
         ++wave_iters;
         ++iter;
 #ifdef QI_DIAG_FAST  // diagnostics: fast steps counted in the cooperative-phase counter
@@ -1191,6 +1252,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       const bool dry_poll = (poll_n++ % (uint32_t)QI_BEST_POLLS) == 0u;
       if (dry_poll && !dry && d == a.seq) {
         dry = true;
+        QI_DIAG_MARK(diag_dry);
         limit = min(limit, steps + a.grace);
         force_at = wave_iters + a.grace;
       }
@@ -1205,9 +1267,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     {
       const bool spill = (has && (steps >= limit || must_spill)) || (!has && fpend && steps >= limit);
       if (__any(spill)) {
+        QI_DIAG_MARK(diag_sp0);
         uint32_t total = 0;
         const uint32_t n = spill ? (has ? 1u : 0u) + (tvalid ? 1u : 0u) + nst + (fpend ? 1u : 0u) : 0u;
         uint32_t slot = reserve<RB>(n, &cc[C_OUT], total);
+        QI_DIAG_MARK(diag_spr);
         if (spill) {
           if (has) write_unit(slot++, T, D, K, depth, dlen, -1);
           if (tvalid) write_entry(slot++, tT, tD, tpk);
@@ -1220,6 +1284,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           has = false;
           done = true;
         }
+#ifdef QI_DIAG_LAUNCH
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        diag_sp1 = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u;
+#endif
       }
     }
     if (!__any(!done)) break;
@@ -1573,6 +1641,17 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     atomicMax(&cc[C_DIAG + 2], t1 - diag_t0);
     atomicMax(&cc[C_DIAG + 3], ~diag_t0);
     atomicMax(&cc[C_DIAG + 4], t1);
+    // phase sums over the waves that went dry and spilled: start -> loop, loop -> dry,
+    // dry -> first spill, spill (slot reservation + unit stores), last spill -> end
+    if (diag_dry && diag_sp0 && diag_sp1) {
+      atomicAdd(&cc[C_DIAG + 5], 1u);
+      atomicAdd(&cc[C_DIAG + 6], diag_loop0 - diag_t0);
+      atomicAdd(&cc[C_DIAG + 7], diag_dry - diag_loop0);
+      atomicAdd(&cc[C_DIAG + 8], diag_sp0 - diag_dry);
+      atomicAdd(&cc[C_DIAG + 9], diag_sp1 - diag_sp0);
+      atomicAdd(&cc[C_DIAG + 10], t1 - diag_sp1);
+      atomicAdd(&cc[C_DIAG + 11], diag_spr - diag_sp0);  // of the spill: waiting for the slot reservation
+    }
   }
 #endif
   // ---- last block of the launch: carry over never-claimed input units (whose waves all
@@ -1609,6 +1688,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
           a.host_ctr[HC_DIAG + 3] = atomicAdd(&cc[C_DIAG + 1], 0u);
           a.host_ctr[HC_DIAG + 4] = atomicAdd(&cc[C_DIAG + 2], 0u);
           a.host_ctr[HC_DIAG + 5] = atomicAdd(&cc[C_DIAG + 4], 0u) + atomicAdd(&cc[C_DIAG + 3], 0u) + 1u;  // end - start
+          for (int q = 0; q < 7; ++q) a.host_ctr[HC_DIAG + 6 + q] = atomicAdd(&cc[C_DIAG + 5 + q], 0u);
         }
       }
 #endif
