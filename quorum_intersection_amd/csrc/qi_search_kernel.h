@@ -590,10 +590,10 @@ constexpr int stamp_bucket(int f) {
 // iteration below carries every rarely needed path; paying for it on every node made the
 // loop issue-bound on control code.
 #ifndef QI_FAST_STEPS
-#define QI_FAST_STEPS 3
+#define QI_FAST_STEPS 12
 #endif
 #ifndef QI_FAST_MIN
-#define QI_FAST_MIN 56
+#define QI_FAST_MIN 28
 #endif
 // run budget for every launch after the first one that had it (see launch_budget): 0 off,
 // 1 always, 2 only while no witness is known (measured: two_tier(8,192) 0.43 / 0.40 / 0.41 ms,
@@ -606,14 +606,6 @@ constexpr int stamp_bucket(int f) {
 #ifndef QI_FAST_MIN_DRY
 #define QI_FAST_MIN_DRY 8
 #endif
-// claim the next units (and flush records) right after the installs instead of after the push
-#ifndef QI_CLAIM_FIRST
-#define QI_CLAIM_FIRST 0
-#endif
-#ifndef QI_FLUSH_AFTER
-#define QI_FLUSH_AFTER 1
-#endif
-
 // TIE: findBestNode's tie rule, fixed per kernel (a run-time choice in the node loop cost
 // 15-50 % per search): false = lowest vertex index, true = the seeded uniform draw.
 template <int MW, int TW, int SMAX, class EV, bool TIE = false>
@@ -980,13 +972,15 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     }
   };
 
-  // Claim the next units for the lanes whose current node is the last thing they hold (no
-  // top entry, empty stack): the unit's loads then have more than one iteration to land
-  // before the install's vmcnt wait.  Indices come from a wave-uniform pool of 64 claimed
-  // with one atomic (a returning atomic per iteration would cost a memory round trip every
-  // iteration).  Convergent.
+  // Claim the next units for the lanes that hold nothing (no node, no top entry, empty
+  // stack), at the start of a full iteration; the units are installed at its end, so their
+  // loads have the whole iteration to land before the install's vmcnt wait.  Indices come
+  // from a wave-uniform pool of 64 claimed with one atomic (a returning atomic per
+  // iteration would cost a memory round trip every iteration).  Convergent.
   auto claim = [&]() {
-    bool want = !done && !fpend && !tvalid && nst == 0 && steps < limit;
+    // (claiming earlier, while a node or stack entries are still held, hoards units: the
+    // queue runs dry sooner, 24 launches instead of 19 and 2.3 vs 1.87 ms per search)
+    bool want = !done && !fpend && !has && !tvalid && nst == 0 && steps < limit;
     uint64_t wm = __ballot(want);
     while (wm) {
       if (pool_next >= pool_end) {
@@ -1023,6 +1017,51 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     }
   };
 
+  // A lane that holds nothing closes its segment (its unit's subtree is done) ...
+  auto close_finished = [&]() {
+    if (!done && !has && !tvalid && seg_open) close_segment();
+  };
+  // ... and installs its claimed unit.
+  auto install_claimed = [&]() {
+    if (!done && !has && !tvalid) {
+      if (seg_open) close_segment();
+      if (fpend && steps < limit) {
+        QI_WAIT_STAMP("vmcnt(0)", F_W_INSTALL);
+        uint32_t UK[MW];
+#pragma unroll
+        for (int w = 0; w < MW; ++w) {
+          T[w] = unit_word(UL::T_ + w);
+          D[w] = unit_word(UL::D_ + w);
+          UK[w] = unit_word(UL::K_ + w);
+        }
+        const uint32_t ud = unit_word(UL::DEPTH);
+        dlen = unit_word(UL::DLEN);
+        const uint32_t nw = (dlen + 3) / 4;
+        if constexpr (OW <= 8) {
+#pragma unroll
+          for (int i = 0; i < OW; ++i)
+            if ((uint32_t)i < nw) DOW_(i) = unit_word(UL::ORD + i);
+        } else {
+          for (uint32_t i = 0; i < nw; ++i) DOW_(i) = unit_word(UL::ORD + (int)i);
+        }
+        fpend = false;
+        ++tot_fetched;
+        seg_idx = fidx;
+        seg_open = true;
+        seg_count = seg_evals = seg_minq = seg_zfb = 0;
+#pragma unroll
+        for (int w = 0; w < MW; ++w) seg_K[w] = K[w] = UK[w];
+        seg_depth = depth = ud;
+        nst = 0;
+        sbase_ = 0;
+        tvalid = false;
+        if (pruned(UK, ud)) close_segment();  // zero record
+        else has = true;
+      }
+    }
+  };
+
+  install_claimed();  // the statically assigned first units
   for (;;) {
     QI_DIAG_MARK(diag_loop0);
 #if QI_FAST_STEPS > 0
@@ -1137,7 +1176,15 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #ifndef QI_NO_FORCE_SPILL
     if (wave_iters >= force_at) limit = 0;
 #endif
-    // ---- (1) lanes without a node: pop the top of stack, else install the next unit ----
+    // Claim units for the lanes that ran out during the fast steps; the loads have this
+    // whole iteration to land: the units are installed at its end, so the lanes go into the
+    // next fast steps with a node.  (Record stores follow the loads: vmcnt counts both in
+    // issue order.)
+    claim();
+    QI_STAMP(F_CLAIM);
+    flush_record();
+    QI_STAMP(F_FLUSH);
+    // ---- (1) lanes without a node: pop the top of stack (units are installed at the end) ----
     if (!done && !has) {
       if (tvalid) {
         const uint32_t b = tpk & 255u, de = (tpk >> 8) & 511u, dle = tpk >> 17;
@@ -1175,56 +1222,11 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
       QI_STAMP(F_POP);
-      if (!has) {
-        if (seg_open) close_segment();  // the unit's subtree is done
-        if (fpend && steps < limit) {  // install the claimed unit
-          QI_WAIT_STAMP("vmcnt(0)", F_W_INSTALL);
-          uint32_t UK[MW];
-#pragma unroll
-          for (int w = 0; w < MW; ++w) {
-            T[w] = unit_word(UL::T_ + w);
-            D[w] = unit_word(UL::D_ + w);
-            UK[w] = unit_word(UL::K_ + w);
-          }
-          const uint32_t ud = unit_word(UL::DEPTH);
-          dlen = unit_word(UL::DLEN);
-          const uint32_t nw = (dlen + 3) / 4;
-          if constexpr (OW <= 8) {
-#pragma unroll
-            for (int i = 0; i < OW; ++i)
-              if ((uint32_t)i < nw) DOW_(i) = unit_word(UL::ORD + i);
-          } else {
-            for (uint32_t i = 0; i < nw; ++i) DOW_(i) = unit_word(UL::ORD + (int)i);
-          }
-          fpend = false;
-          ++tot_fetched;
-          seg_idx = fidx;
-          seg_open = true;
-          seg_count = seg_evals = seg_minq = seg_zfb = 0;
-#pragma unroll
-          for (int w = 0; w < MW; ++w) seg_K[w] = K[w] = UK[w];
-          seg_depth = depth = ud;
-          nst = 0;
-          sbase_ = 0;
-          tvalid = false;
-          if (pruned(UK, ud)) close_segment();  // zero record
-          else has = true;
-        }
-      }
     }
-
+    // (a lane that finished during the fast steps may be found done just below: its
+    // segment closes here)
+    close_finished();
     QI_STAMP(F_INSTALL);
-#if QI_CLAIM_FIRST
-    // Claim right after the installs: a lane that now holds only its node (or nothing) will
-    // need a unit next, and the unit's loads get this whole iteration to land.  vmcnt
-    // counts loads and stores in issue order and the compiler drains it before the claim's
-    // loads (their destination registers are loop-carried): here that drain finds only
-    // operations a full iteration old, and the record stores follow the loads.
-    claim();
-    QI_STAMP(F_CLAIM);
-    flush_record();
-    QI_STAMP(F_FLUSH);
-#endif
     // a lane with nothing left is done once it cannot get a unit any more (a claimed unit
     // past the budget is spilled below)
     if (!has && !tvalid && nst == 0 && !fpend && (steps >= limit || pool_dead)) done = true;
@@ -1394,22 +1396,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
 
-    // the unit loads of lanes that became free: in flight during the quorum-leaf phase
-    // below (the install waits on vmcnt, which counts stores and loads in issue order)
     QI_STAMP(F_PUSH);
-#if !QI_CLAIM_FIRST
-#if QI_FLUSH_AFTER
-    claim();
-    QI_STAMP(F_CLAIM);
-    flush_record();
-    QI_STAMP(F_FLUSH);
-#else
-    flush_record();
-    QI_STAMP(F_FLUSH);
-    claim();
-    QI_STAMP(F_CLAIM);
-#endif
-#endif
     // ---- (5) quorum leaves: isMinimalQuorum + visitor ---------------------------------
     // Quorum leaves with |D| - 1 < qmin: no D \ {v} can hold a quorum (LocalFlat::qmin),
     // so D is minimal without evaluating them (still credited, as the reference makes the
@@ -1575,12 +1562,10 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         }
       }
       __syncthreads();
-#if !QI_CLAIM_FIRST
-      flush_record();  // lanes freed by the cooperative phase
-      claim();
-#endif
     }
     QI_STAMP(F_COOP);
+    install_claimed();
+    QI_STAMP(F_INSTALL);
   }
   flush_record();
 
