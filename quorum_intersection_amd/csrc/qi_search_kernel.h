@@ -570,19 +570,21 @@ constexpr int stamp_bucket(int f) {
 #ifndef QI_LDS_OW
 #define QI_LDS_OW 0
 #endif
-// Iterations (fast steps included) between polls of the global queue head and the
-// device-side best key.  A wave with an idle lane learns that the queue is dry from its own
-// failed claim; the poll only ends waves whose lanes are all still busy, and ending those
-// early costs more (spilled stacks, extra launches) than it saves: on the bench workload
-// 192 / 256 / 384 / 512 / 1024 iterations gave 2.61 / 2.48 / 2.22 / 2.25 / 2.32 ms.
+// Iterations (fast steps included) between polls of the dry flag (the poll is taken in the
+// first full iteration past the interval).  A wave with an empty lane learns that the queue
+// is dry from its own failed claim; the poll ends the waves whose lanes are all still busy.
+// With every lane's unit turnover paid per full iteration (not per node) the waves of a
+// launch should end together: 768 / 576 / 384 / 192 / 128 / 96 / 64 / 32 iterations gave
+// 1.74 / 1.69 / 1.62 / 1.59 / 1.55 / 1.49-1.51 / 1.51 / 1.50 ms per search (before the fast
+// steps the optimum was 384: ending busy waves early cost more in unit turnover).
 #ifndef QI_POLL_EVERY
-#define QI_POLL_EVERY 384
+#define QI_POLL_EVERY 96
 #endif
 // The best key is polled more often than the dry flag acts: every QI_POLL_EVERY /
 // QI_BEST_POLLS iterations (a witness found elsewhere prunes sooner); the dry flag counts in
 // every QI_BEST_POLLS-th of these polls.
 #ifndef QI_BEST_POLLS
-#define QI_BEST_POLLS 6
+#define QI_BEST_POLLS 2
 #endif
 // Fast steps: up to QI_FAST_STEPS lean iterations run between two full ones while at least
 // QI_FAST_MIN lanes can pop or process a node without any service (no unit to install, no
@@ -1077,6 +1079,22 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         if ((uint32_t)__popcll(__ballot(elig)) < (dry ? (uint32_t)QI_FAST_MIN_DRY : (uint32_t)QI_FAST_MIN)) break;
         ++wave_iters;
         ++iter;
+#ifdef QI_PAD_V  // diagnostics: extra independent VALU / SALU instructions per fast step
+        {
+          uint32_t pv = lane;
+#pragma unroll
+          for (int q = 0; q < QI_PAD_V; ++q) asm volatile("v_xor_b32 %0, 0x55, %0" : "+v"(pv));
+          asm volatile("" ::"v"(pv));
+        }
+#endif
+#ifdef QI_PAD_S
+        {
+          uint32_t ps = iter;
+#pragma unroll
+          for (int q = 0; q < QI_PAD_S; ++q) asm volatile("s_xor_b32 %0, %0, 0x55" : "+s"(ps));
+          asm volatile("" ::"s"(ps));
+        }
+#endif
 #ifdef QI_DIAG_FAST  // diagnostics: fast steps counted in the cooperative-phase counter
         ++coop_phases;
 #endif
@@ -1176,6 +1194,42 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #ifndef QI_NO_FORCE_SPILL
     if (wave_iters >= force_at) limit = 0;
 #endif
+    // (Before the claim: the compiler waits for every outstanding load where it copies the
+    // polled registers, which after the claim would include the unit loads just issued.)
+    // Poll this wave's line (loads issued one full iteration ahead): the best key, and
+    // whether a wave sharing the line found the unit queue dry.  Once no unit is left to
+    // claim, every lane gets a short grace period and then spills: the next launch spreads
+    // the remaining subtrees over all lanes instead of letting a few lanes grind through
+    // deep subtrees while the rest idle.
+    if (poll_issued && iter >= next_poll) {
+      poll_issued = false;
+      next_poll = iter + (uint32_t)(QI_POLL_EVERY / QI_BEST_POLLS);
+      uint32_t d = 0;
+      uint64_t b = ~0ull;
+      if (lane == 0) {
+        d = poll_d;
+        b = poll_b;
+        if (forwarder && poll_x < b) {  // a key from another engine: into this device's words
+          b = poll_x;
+          publish_best(poll_x);
+        }
+      }
+      d = lane0(d);
+      best64 = lane0(b);
+      const bool dry_poll = (poll_n++ % (uint32_t)QI_BEST_POLLS) == 0u;
+      if (dry_poll && !dry && d == a.seq) {
+        dry = true;
+        QI_DIAG_MARK(diag_dry);
+        limit = min(limit, steps + a.grace);
+        force_at = wave_iters + a.grace;
+      }
+    } else if (!poll_issued && iter + 2u * ((uint32_t)QI_FAST_STEPS + 1u) >= next_poll) {
+      // at least one full iteration before the poll that reads them
+      poll_issued = true;
+      if (lane == 0) issue_poll();
+    }
+    ++iter;
+    QI_STAMP(F_POLL);
     // Claim units for the lanes that ran out during the fast steps; the loads have this
     // whole iteration to land: the units are installed at its end, so the lanes go into the
     // next fast steps with a node.  (Record stores follow the loads: vmcnt counts both in
@@ -1231,40 +1285,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // past the budget is spilled below)
     if (!has && !tvalid && nst == 0 && !fpend && (steps >= limit || pool_dead)) done = true;
 
-    // Poll this wave's line (loads issued one full iteration ahead): the best key, and
-    // whether a wave sharing the line found the unit queue dry.  Once no unit is left to
-    // claim, every lane gets a short grace period and then spills: the next launch spreads
-    // the remaining subtrees over all lanes instead of letting a few lanes grind through
-    // deep subtrees while the rest idle.
-    if (poll_issued && iter >= next_poll) {
-      poll_issued = false;
-      next_poll = iter + (uint32_t)(QI_POLL_EVERY / QI_BEST_POLLS);
-      uint32_t d = 0;
-      uint64_t b = ~0ull;
-      if (lane == 0) {
-        d = poll_d;
-        b = poll_b;
-        if (forwarder && poll_x < b) {  // a key from another engine: into this device's words
-          b = poll_x;
-          publish_best(poll_x);
-        }
-      }
-      d = lane0(d);
-      best64 = lane0(b);
-      const bool dry_poll = (poll_n++ % (uint32_t)QI_BEST_POLLS) == 0u;
-      if (dry_poll && !dry && d == a.seq) {
-        dry = true;
-        QI_DIAG_MARK(diag_dry);
-        limit = min(limit, steps + a.grace);
-        force_at = wave_iters + a.grace;
-      }
-    } else if (!poll_issued && iter + 2u * ((uint32_t)QI_FAST_STEPS + 1u) >= next_poll) {
-      // at least one full iteration before the poll that reads them
-      poll_issued = true;
-      if (lane == 0) issue_poll();
-    }
-    ++iter;
-    QI_STAMP(F_POLL);
     // ---- (3) budget exhausted: spill current node, top, stack and claimed unit ---------
     {
       const bool spill = (has && (steps >= limit || must_spill)) || (!has && fpend && steps >= limit);
