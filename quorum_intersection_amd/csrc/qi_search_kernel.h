@@ -446,6 +446,10 @@ __device__ __forceinline__ bool after_key(const uint32_t (&K)[MW], uint32_t d, c
 template <int MW>
 __device__ __forceinline__ void key_prefix_bit(uint32_t (&K)[MW], uint32_t de) {
   // keep path positions < de, then set position de (inclusion branch at depth de)
+  if constexpr (MW == 1) {  // de <= 31: three shifts and a merge
+    K[0] = (K[0] & ~(0xFFFFFFFFu >> de)) | (0x80000000u >> de);
+    return;
+  }
 #pragma unroll
   for (int w = 0; w < MW; ++w) {
     const uint32_t lo = (uint32_t)w * 32u;
@@ -736,7 +740,8 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   for (int q = 0; q < FW; ++q) fdat[q] = 0;
   // current segment (one per installed unit)
   bool seg_open = false;
-  uint32_t seg_idx = 0, seg_depth = 0, seg_count = 0, seg_evals = 0, seg_minq = 0, seg_zfb = 0;
+  uint32_t seg_idx = 0, seg_depth = 0, seg_evals = 0, seg_minq = 0, seg_zfb = 0;
+  uint32_t seg_s0 = 0;  // the lane's step count when the segment opened: its nodes = steps - seg_s0
   uint32_t seg_K[MW];
 #pragma unroll
   for (int w = 0; w < MW; ++w) seg_K[w] = 0;
@@ -828,6 +833,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll
     for (int w = 0; w < MW; ++w) rec[w] = seg_K[w];
     rec[MW] = seg_depth;
+    const uint32_t seg_count = steps - seg_s0;
     rec[MW + 1] = seg_count;
     rec[MW + 2] = seg_evals;
     rec[MW + 3] = seg_minq;
@@ -1050,15 +1056,17 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         ++tot_fetched;
         seg_idx = fidx;
         seg_open = true;
-        seg_count = seg_evals = seg_minq = seg_zfb = 0;
+        seg_s0 = steps;
+        seg_evals = seg_minq = seg_zfb = 0;
 #pragma unroll
         for (int w = 0; w < MW; ++w) seg_K[w] = K[w] = UK[w];
         seg_depth = depth = ud;
         nst = 0;
         sbase_ = 0;
         tvalid = false;
-        if (pruned(UK, ud)) close_segment();  // zero record
-        else has = true;
+        // a unit past the best witness keeps its open, empty segment: the next close writes
+        // its zero record
+        has = !pruned(UK, ud);
       }
     }
   };
@@ -1143,7 +1151,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         const bool qne = EV::template gfp<0>(f, X, 0u, rounds);  // cpp:301
         if (go) {
           ++steps;
-          ++seg_count;
           if (leaf0) has = false;
         }
         if (ev2) {
@@ -1321,7 +1328,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     bool active = has;
     if (active) {
       ++steps;
-      ++seg_count;
       uint32_t any = 0;
 #pragma unroll
       for (int w = 0; w < MW; ++w) any |= T[w] | D[w];
