@@ -332,13 +332,9 @@ struct WitLayout {
 // final block to pinned host memory (HC_* words), where the host polls it.
 enum : int {
   C_OUT = 0,       // units written to units_out (spills + carried-over units)   [atomic]
-#ifdef QI_CTR_PACKED  // diagnostics: the four atomic words on one line
-  C_HEAD = 1, C_DONE = 2, C_EVX = 4,
-#else
   C_HEAD = 32,     // dynamic claims past the statically assigned range           [atomic]
   C_DONE = 64,     // used blocks that finished                                   [atomic]
   C_EVX = 96,      // stack evictions granted from the shared output pool          [atomic]
-#endif
   C_DIAG = 100,    // QI_DIAG_LAUNCH: max wave iterations, sum / max wave ticks, max ~start, max end [atomic]
   C_NIN = 128,     // input units of this launch (the previous block's C_OUT)
   C_LOGB = 129,    // first segment-log record of this launch
@@ -632,11 +628,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   // loaded when installed
   constexpr bool PREFETCH = UW <= 20;
   constexpr int FW = PREFETCH ? UW : 4;
-#ifdef QI_WORD_STORES  // diagnostics: units and records leave word by word
-  constexpr bool WIDE = false;
-#else
-  constexpr bool WIDE = PREFETCH;
-#endif
+  constexpr bool WIDE = PREFETCH;  // small units and their records leave as 16- / 8-byte stores
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* st = lds;                                          // [SMAX][SE][64]
   uint32_t* co_NE = st + SMAX * SE * WAVE;                      // [MW][64] per pending rank
@@ -815,7 +807,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   for (int w = 0; w < RL::WORDS; ++w) rec[w] = 0;
   auto flush_record = [&]() {
     if (rec_pend) {
-#ifndef QI_ABL_NOREC  // diagnostics: no record stores (counts then only via the running totals)
       uint32_t* r = records + (size_t)rec_idx * RL::WORDS;
       if constexpr (WIDE && RL::WORDS % 2 == 0) {  // 8-byte stores (record stride and log base are 8-byte multiples)
 #pragma unroll
@@ -824,7 +815,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #pragma unroll
         for (int w = 0; w < RL::WORDS; ++w) r[w] = rec[w];
       }
-#endif
       rec_pend = false;
     }
   };
@@ -1074,7 +1064,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   install_claimed();  // the statically assigned first units
   for (;;) {
     QI_DIAG_MARK(diag_loop0);
-#if QI_FAST_STEPS > 0
     // ---- (0) fast steps: pop or process one node per lane, common outcomes only --------
     // A lane whose node is a quorum leaf (cpp:281) or whose push would need an eviction is
     // held, uncommitted, for the full iteration; lanes without node and stack wait there too.
@@ -1087,22 +1076,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         if ((uint32_t)__popcll(__ballot(elig)) < (dry ? (uint32_t)QI_FAST_MIN_DRY : (uint32_t)QI_FAST_MIN)) break;
         ++wave_iters;
         ++iter;
-#ifdef QI_PAD_V  // diagnostics: extra independent VALU / SALU instructions per fast step
-        {
-          uint32_t pv = lane;
-#pragma unroll
-          for (int q = 0; q < QI_PAD_V; ++q) asm volatile("v_xor_b32 %0, 0x55, %0" : "+v"(pv));
-          asm volatile("" ::"v"(pv));
-        }
-#endif
-#ifdef QI_PAD_S
-        {
-          uint32_t ps = iter;
-#pragma unroll
-          for (int q = 0; q < QI_PAD_S; ++q) asm volatile("s_xor_b32 %0, %0, 0x55" : "+s"(ps));
-          asm volatile("" ::"s"(ps));
-        }
-#endif
 #ifdef QI_DIAG_FAST  // diagnostics: fast steps counted in the cooperative-phase counter
         ++coop_phases;
 #endif
@@ -1195,12 +1168,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       }
     }
     QI_STAMP(F_FAST);
-#endif
     // the grace period of a dry wave is over: every lane spills in this iteration (per-lane
     // step limits alone would let lanes that idled during the grace period lag behind)
-#ifndef QI_NO_FORCE_SPILL
     if (wave_iters >= force_at) limit = 0;
-#endif
     // (Before the claim: the compiler waits for every outstanding load where it copies the
     // polled registers, which after the claim would include the unit loads just issued.)
     // Poll this wave's line (loads issued one full iteration ahead): the best key, and
