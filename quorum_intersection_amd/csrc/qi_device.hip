@@ -76,27 +76,6 @@ __global__ __launch_bounds__(64) void ordered_kernel(OrdArgs oa) {
   ordered_body<MW, TW>(oa);
 }
 
-// Fold a host-known best witness into the device-side one and its polled replicas (1-word keys).
-static __global__ void min_best_kernel(unsigned long long* best64, uint32_t* poll_rep, unsigned long long v) {
-  if (threadIdx.x == 0) atomicMin(best64, v);
-  if (threadIdx.x < POLL_REPS) atomicMin((unsigned long long*)(poll_rep + (size_t)threadIdx.x * 32), v);
-}
-
-// A rank's share of a broadcast frontier, dealt in rounds of `stride` units with a rotating
-// offset: out[q] = in[q * stride + (offset - q) mod stride].  (A plain stride keeps any
-// period of the frontier order that divides it: spilled stacks alternate size classes, and
-// stride 8 once gave ranks 10 M vs 19 M nodes.)
-template <int WORDS>
-__global__ void gather_units_kernel(const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt, uint32_t* out) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t src = i * stride + (offset + stride - i % stride) % stride;
-    const uint4* s4 = (const uint4*)(in + src * WORDS);
-    uint4* d4 = (uint4*)(out + i * WORDS);
-#pragma unroll
-    for (int q = 0; q < WORDS / 4; ++q) d4[q] = s4[q];
-  }
-}
-
 // frontier sort helpers (SearchDeviceImpl::sort_frontier)
 static __global__ void iota_kernel(uint32_t* p, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -114,40 +93,6 @@ __global__ void gather_perm_kernel(const uint32_t* in, const uint32_t* perm, uin
     uint4* d4 = (uint4*)(out + i * WORDS);
 #pragma unroll
     for (int q = 0; q < WORDS / 4; ++q) d4[q] = s4[q];
-  }
-}
-
-// Preorder-filtered sums over a log chunk: segment roots at or before (key, depth).
-// Wave shuffles, then one LDS combine per block and one atomic per value per block (a
-// same-address atomic per wave serialised ~65K atomics at the L2: 0.53 ms per reduce).
-template <int MW>
-__global__ __launch_bounds__(256) void reduce_kernel(const uint32_t* records, uint64_t n, uint32_t has_key,
-                                                     const uint32_t* key, uint32_t depth, unsigned long long* out) {
-  __shared__ unsigned long long part[4][4];
-  uint64_t s[4] = {0, 0, 0, 0};
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t* r = records + i * RecLayout<MW>::WORDS;
-    uint32_t K[MW];
-#pragma unroll
-    for (int w = 0; w < MW; ++w) K[w] = r[w];
-    if (has_key && after_key<MW>(K, r[MW], key, depth)) continue;
-    s[0] += r[MW + 1];
-    s[1] += r[MW + 2];
-    s[2] += r[MW + 3];
-    s[3] += r[MW + 4];
-  }
-  const uint32_t wv = threadIdx.x >> 6;
-  for (int q = 0; q < 4; ++q) {
-    uint64_t v = s[q];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    if ((threadIdx.x & 63) == 0) part[wv][q] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    unsigned long long v = 0;
-    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) v += part[w][threadIdx.x];
-    if (v) atomicAdd(&out[threadIdx.x], v);
   }
 }
 
@@ -396,21 +341,94 @@ bool enable_peer(int a, int b) {
 }
 #endif  // QI_PART <= 0
 
-namespace {
-
-// Stack levels of the run-time specialised kernel for a template shape.  |SCC| <= 32: 20
-// levels leave LDS for 9 resident waves per CU instead of 8 (17,408 B per wave).  Measured
-// on the bench workload: 24 / 22 / 21 / 20 / 19 / 14 levels = 8 / 8 / 8 / 9 / 9 / 12 waves gave
-// 2.63 / 2.62 / 2.55 / 2.39 / 2.38 / 2.48 ms; below 19 the extra stack evictions cost more
-// than the waves bring.  The engine and jit_precompile must agree (the cache key is the source).
-inline int jit_default_smax(int MW, int SMAX) {
-  int s = MW == 1 ? 20 : SMAX;
-  if (const char* e = std::getenv("QI_JIT_SMAX")) s = std::max(4, std::min(64, std::atoi(e)));  // diagnostics
-  return s;
+// Small kernels every engine shape uses (reduce, best-key fold, strided deal): defined in ONE
+// part of this file and launched through these wrappers.  As per-shape template instances they
+// lived in each part's code object, so a search on the run-time specialised kernel that ended
+// with a witness loaded a whole part (4-5 ms) just to run its reduce.
+void launch_reduce(uint32_t mw, const uint32_t* records, uint64_t n, uint32_t has_key, const uint32_t* key, uint32_t depth,
+                   unsigned long long* out, uint32_t blocks, hipStream_t s);
+void launch_min_best(unsigned long long* best64, uint32_t* poll_rep, unsigned long long v, hipStream_t s);
+void launch_gather_units(uint32_t words, const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt, uint32_t* out,
+                         uint32_t blocks, hipStream_t s);
+#if QI_PART <= 0
+namespace dev {
+// Fold a host-known best witness into the device-side one and its polled replicas (1-word keys).
+static __global__ void min_best_kernel(unsigned long long* best64, uint32_t* poll_rep, unsigned long long v) {
+  if (threadIdx.x == 0) atomicMin(best64, v);
+  if (threadIdx.x < POLL_REPS) atomicMin((unsigned long long*)(poll_rep + (size_t)threadIdx.x * 32), v);
 }
 
-// hipStreamCreate costs ~2 ms on this stack (measured, QI_TRACE): engines take their stream
-// from a per-device pool and return it, so a solve does not pay it twice.
+// A rank's share of a broadcast frontier, dealt in rounds of `stride` units with a rotating
+// offset: out[q] = in[q * stride + (offset - q) mod stride].  (A plain stride keeps any
+// period of the frontier order that divides it: spilled stacks alternate size classes, and
+// stride 8 once gave ranks 10 M vs 19 M nodes.)  `words` per unit, a multiple of 4.
+static __global__ void gather_units_kernel(uint32_t words, const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt,
+                                           uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cnt; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t src = i * stride + (offset + stride - i % stride) % stride;
+    const uint4* s4 = (const uint4*)(in + src * words);
+    uint4* d4 = (uint4*)(out + i * words);
+    for (uint32_t q = 0; q < words / 4; ++q) d4[q] = s4[q];
+  }
+}
+
+// Preorder-filtered sums over a log chunk: segment roots at or before (key, depth); records
+// of mw key words + depth, count, evals, minq, zero_fallback (RecLayout).  Wave shuffles, then
+// one LDS combine per block and one atomic per value per block (a same-address atomic per
+// wave serialised ~65K atomics at the L2: 0.53 ms per reduce).
+static __global__ __launch_bounds__(256) void reduce_kernel(uint32_t mw, const uint32_t* records, uint64_t n, uint32_t has_key,
+                                                            const uint32_t* key, uint32_t depth, unsigned long long* out) {
+  __shared__ unsigned long long part[4][4];
+  uint64_t s[4] = {0, 0, 0, 0};
+  const uint32_t rw = mw + 5;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t* r = records + i * rw;
+    if (has_key) {  // preorder "strictly after": padded path bits, then depth
+      bool after = r[mw] > depth;
+      for (uint32_t w = mw; w-- > 0;)
+        if (r[w] != key[w]) after = r[w] > key[w];
+      if (after) continue;
+    }
+    s[0] += r[mw + 1];
+    s[1] += r[mw + 2];
+    s[2] += r[mw + 3];
+    s[3] += r[mw + 4];
+  }
+  const uint32_t wv = threadIdx.x >> 6;
+  for (int q = 0; q < 4; ++q) {
+    uint64_t v = s[q];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    if ((threadIdx.x & 63) == 0) part[wv][q] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    unsigned long long v = 0;
+    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) v += part[w][threadIdx.x];
+    if (v) atomicAdd(&out[threadIdx.x], v);
+  }
+}
+}  // namespace dev
+void launch_reduce(uint32_t mw, const uint32_t* records, uint64_t n, uint32_t has_key, const uint32_t* key, uint32_t depth,
+                   unsigned long long* out, uint32_t blocks, hipStream_t s) {
+  hipLaunchKernelGGL(dev::reduce_kernel, dim3(blocks), dim3(256), 0, s, mw, records, n, has_key, key, depth, out);
+}
+void launch_min_best(unsigned long long* best64, uint32_t* poll_rep, unsigned long long v, hipStream_t s) {
+  hipLaunchKernelGGL(dev::min_best_kernel, dim3(1), dim3(64), 0, s, best64, poll_rep, v);
+}
+void launch_gather_units(uint32_t words, const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt, uint32_t* out,
+                         uint32_t blocks, hipStream_t s) {
+  hipLaunchKernelGGL(dev::gather_units_kernel, dim3(blocks), dim3(256), 0, s, words, in, offset, stride, cnt, out);
+}
+#endif  // QI_PART <= 0
+
+// hipStreamCreate costs ~2.4 ms on this stack (measured, QI_TRACE; the first one of a process
+// far more): engines and the per-SCC checker take their stream from ONE per-device pool and
+// return it, so a solve creates none.  The pool is defined in one part of this file only:
+// an instance per part gave every engine shape an empty pool of its own.
+hipStream_t acquire_stream(int device);
+void release_stream(int device, hipStream_t s);
+#if QI_PART <= 0
 struct StreamPool {
   std::mutex mu;
   std::vector<std::pair<int, hipStream_t>> free;
@@ -431,7 +449,11 @@ hipStream_t acquire_stream(int device) {
       }
   }
   hipStream_t s = nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
   HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  if (std::getenv("QI_TRACE"))
+    std::fprintf(stderr, "[qi]   hipStreamCreate (device %d): %.3f ms\n", device,
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return s;
 }
 void release_stream(int device, hipStream_t s) {
@@ -439,6 +461,56 @@ void release_stream(int device, hipStream_t s) {
   (void)hipStreamSynchronize(s);
   std::lock_guard<std::mutex> g(stream_pool().mu);
   stream_pool().free.emplace_back(device, s);
+}
+// Pinned staging buffers of the per-SCC checker, pooled the same way: the first
+// hipHostMalloc of a process beyond a few KB cost 5-6 ms inside the first solve (a
+// 512-validator network's 31 KB against 7 KB for 256 validators).  device_prepare creates
+// one of kStageMin bytes with the device.
+constexpr size_t kStageMin = 256u << 10;
+struct StagePool {
+  std::mutex mu;
+  std::vector<std::pair<unsigned long long*, size_t>> free;  // (buffer, bytes)
+};
+StagePool& stage_pool() {
+  static StagePool* p = new StagePool;  // leaked on purpose, like the streams
+  return *p;
+}
+unsigned long long* acquire_stage(size_t bytes, size_t* cap) {
+  {
+    std::lock_guard<std::mutex> g(stage_pool().mu);
+    auto& fr = stage_pool().free;
+    for (size_t i = 0; i < fr.size(); ++i)
+      if (fr[i].second >= bytes) {
+        unsigned long long* b = fr[i].first;
+        *cap = fr[i].second;
+        fr.erase(fr.begin() + (long)i);
+        return b;
+      }
+  }
+  const size_t want = std::max(bytes, kStageMin);
+  unsigned long long* b = nullptr;
+  HIP_CHECK(hipHostMalloc((void**)&b, want, hipHostMallocPortable));
+  *cap = want;
+  return b;
+}
+void release_stage(unsigned long long* b, size_t cap) {
+  if (!b) return;
+  std::lock_guard<std::mutex> g(stage_pool().mu);
+  stage_pool().free.emplace_back(b, cap);
+}
+#endif  // QI_PART <= 0
+
+namespace {
+
+// Stack levels of the run-time specialised kernel for a template shape.  |SCC| <= 32: 20
+// levels leave LDS for 9 resident waves per CU instead of 8 (17,408 B per wave).  Measured
+// on the bench workload: 24 / 22 / 21 / 20 / 19 / 14 levels = 8 / 8 / 8 / 9 / 9 / 12 waves gave
+// 2.63 / 2.62 / 2.55 / 2.39 / 2.38 / 2.48 ms; below 19 the extra stack evictions cost more
+// than the waves bring.  The engine and jit_precompile must agree (the cache key is the source).
+inline int jit_default_smax(int MW, int SMAX) {
+  int s = MW == 1 ? 20 : SMAX;
+  if (const char* e = std::getenv("QI_JIT_SMAX")) s = std::max(4, std::min(64, std::atoi(e)));  // diagnostics
+  return s;
 }
 
 template <typename T>
@@ -519,7 +591,7 @@ class GfpDeviceImpl : public GfpDevice {
     (void)hipFree(rounds_);
     (void)hipFree(io_);
     (void)hipFree(scratch_);
-    if (hio_) (void)hipHostFree(hio_);
+    release_stage(hio_, hio_bytes_);
     (void)hipEventDestroy(e0_);
     (void)hipEventDestroy(e1_);
     release_stream(device_, stream_);
@@ -535,22 +607,38 @@ class GfpDeviceImpl : public GfpDevice {
   void run(const uint64_t* nodes, const uint64_t* avail, uint32_t count, uint64_t* out) override {
     if (count == 0) return;
     DeviceGuard dg(device_);
+    auto tc0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {  // QI_TIMING: where a batch's host time goes
+      if (!timing::enabled()) return;
+      const auto now = std::chrono::steady_clock::now();
+      timing::add((std::string("gfp_run_") + what).c_str(), std::chrono::duration<double, std::milli>(now - tc0).count());
+      tc0 = now;
+    };
     StreamLease lease(*this);
+    lap("stream");
     const size_t per = (size_t)count * d_.words;
-    if (io_cap_ < per) {
+    if (io_cap_ < per && 3 * per * 8 > kZeroCopyBytes) {
       (void)hipFree(io_);
-      if (hio_) (void)hipHostFree(hio_);
       io_ = dalloc<unsigned long long>(3 * per);
-      HIP_CHECK(hipHostMalloc((void**)&hio_, 3 * per * 8, hipHostMallocDefault));
       io_cap_ = per;
     }
-    unsigned long long* dn = io_;
-    unsigned long long* da = io_ + per;
-    unsigned long long* dout = io_ + 2 * per;
+    if (hio_bytes_ < 3 * per * 8) {
+      release_stage(hio_, hio_bytes_);
+      hio_ = acquire_stage(3 * per * 8, &hio_bytes_);
+      HIP_CHECK(hipHostGetDevicePointer((void**)&hio_dev_, hio_, 0));
+    }
+    // A small batch (the per-SCC checks of a solve) is read and written by the kernel
+    // straight in the pinned buffer: the first hipMemcpyAsync of a process beyond ~16 KB
+    // brings up a copy queue (5.6 ms inside the first solve of a 512-validator network).
+    const bool zero_copy = 3 * per * 8 <= kZeroCopyBytes;
+    lap("buffers");
+    unsigned long long* dn = zero_copy ? hio_dev_ : io_;
+    unsigned long long* da = dn + per;
+    unsigned long long* dout = dn + 2 * per;
     // both inputs through one pinned staging buffer: one DMA each way per batch
     std::memcpy(hio_, nodes, per * 8);
     std::memcpy(hio_ + per, avail, per * 8);
-    HIP_CHECK(hipMemcpyAsync(dn, hio_, 2 * per * 8, hipMemcpyHostToDevice, stream_));
+    if (!zero_copy) HIP_CHECK(hipMemcpyAsync(dn, hio_, 2 * per * 8, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemsetAsync(rounds_, 0, 8, stream_));
     const size_t shm = (size_t)d_.words * 16 + ((d_.T + 15) / 16) * 16;
     HIP_CHECK(hipEventRecord(e0_, stream_));
@@ -569,8 +657,10 @@ class GfpDeviceImpl : public GfpDevice {
     }
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipEventRecord(e1_, stream_));
-    HIP_CHECK(hipMemcpyAsync(hio_ + 2 * per, dout, per * 8, hipMemcpyDeviceToHost, stream_));
+    if (!zero_copy) HIP_CHECK(hipMemcpyAsync(hio_ + 2 * per, dout, per * 8, hipMemcpyDeviceToHost, stream_));
+    lap("enqueue");
     HIP_CHECK(hipStreamSynchronize(stream_));
+    lap("sync");
     std::memcpy(out, hio_ + 2 * per, per * 8);
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, e0_, e1_));
@@ -621,7 +711,10 @@ class GfpDeviceImpl : public GfpDevice {
   std::vector<const uint32_t*> bufs_;
   unsigned long long* rounds_ = nullptr;
   unsigned long long* io_ = nullptr;
-  unsigned long long* hio_ = nullptr;  // pinned staging: nodes, avail, out
+  unsigned long long* hio_ = nullptr;  // pinned staging (pooled): nodes, avail, out
+  size_t hio_bytes_ = 0;
+  unsigned long long* hio_dev_ = nullptr;  // the same buffer as the device sees it
+  static constexpr size_t kZeroCopyBytes = 64u << 10;
   size_t io_cap_ = 0;
   uint8_t* scratch_ = nullptr;  // global-memory query state (networks beyond the LDS image)
   size_t scratch_cap_ = 0;
@@ -920,8 +1013,7 @@ class SearchDeviceImpl : public SearchDevice {
     static_assert(MW <= dev::KEY_WORDS_MAX, "path key wider than the key buffers");
     for (int w = 0; w < dev::KEY_WORDS_MAX; ++w) a.best_key[w] = w < (int)best_key_.size() ? best_key_[w] : 0u;
     if (MW == 1 && has_best_ && best_dirty_) {  // 1-word keys: the device best is exact; fold the host's in
-      hipLaunchKernelGGL(dev::min_best_kernel, dim3(1), dim3(64), 0, stream_, best64_, poll_rep_,
-                         ((unsigned long long)best_key_[0] << 32) | best_depth_);
+      launch_min_best(best64_, poll_rep_, ((unsigned long long)best_key_[0] << 32) | best_depth_, stream_);
       HIP_CHECK(hipGetLastError());
     }
     best_dirty_ = false;
@@ -1177,8 +1269,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (cnt) {
       ensure_cap(1 - cur_, cnt);
       const uint32_t nb = (uint32_t)std::min<uint64_t>((cnt + 255) / 256, 4096);
-      hipLaunchKernelGGL(dev::gather_units_kernel<UL::WORDS>, dim3(nb), dim3(256), 0, stream_, units_[cur_], offset, stride,
-                         cnt, units_[1 - cur_]);
+      launch_gather_units((uint32_t)UL::WORDS, units_[cur_], offset, stride, cnt, units_[1 - cur_], nb, stream_);
       HIP_CHECK(hipGetLastError());
       cur_ = 1 - cur_;
     }
@@ -1234,8 +1325,8 @@ class SearchDeviceImpl : public SearchDevice {
     for (auto& c : log_) {
       if (!c.used) continue;
       const uint32_t nb = (uint32_t)std::min<uint64_t>((c.used + 255) / 256, (uint64_t)cus_ * 4u);
-      hipLaunchKernelGGL(dev::reduce_kernel<MW>, dim3(nb), dim3(256), 0, stream_, c.ptr, c.used, has_key ? 1u : 0u,
-                         keydev_, depth, red_);
+      static_assert(RL::WORDS == MW + 5, "reduce_kernel's record layout");
+      launch_reduce((uint32_t)MW, c.ptr, c.used, has_key ? 1u : 0u, keydev_, depth, red_, nb, stream_);
       HIP_CHECK(hipGetLastError());
     }
     unsigned long long r[4];
@@ -1581,7 +1672,12 @@ uint32_t hash_iteration_order(const uint32_t* keys, uint32_t n_keys, const uint3
 
 void device_prepare(int device) {
   DeviceGuard dg(device);
+  // the stream (hardware queue) that the per-SCC checks and the search engine of a solve
+  // take in turn is created here, with the device, not inside the first solve
   release_stream(device, acquire_stream(device));
+  size_t cap = 0;
+  unsigned long long* st = acquire_stage(kStageMin, &cap);  // the per-SCC checker's pinned staging buffer
+  release_stage(st, cap);
   (void)static_scratch_ptr(device);
 }
 
