@@ -38,10 +38,11 @@
 #include "qi_jit.h"
 #include "../../include/quorum_intersection.h"
 
-// The Makefile compiles this file in parts (-DQI_PART=0..4) so the kernel instantiations
-// build in parallel: part 0 holds everything except the search engines, parts 1-4 one group
-// of SearchDeviceImpl instantiations each (make_engine below).  Without QI_PART the file is
-// one translation unit.
+// The Makefile compiles this file in parts (-DQI_PART=0..6) so the kernel instantiations
+// build in parallel and load separately (a part is a code object, loaded at its first
+// launch): part 0 holds everything except the search engines, parts 1-5 one group of
+// SearchDeviceImpl instantiations each (make_engine below), part 6 the frontier sort.
+// Without QI_PART the file is one translation unit.
 #ifndef QI_PART
 #define QI_PART -1
 #endif
@@ -74,26 +75,6 @@ __global__ __launch_bounds__(64) void search_kernel(SearchArgs a) {
 template <int MW, int TW>
 __global__ __launch_bounds__(64) void ordered_kernel(OrdArgs oa) {
   ordered_body<MW, TW>(oa);
-}
-
-// frontier sort helpers (SearchDeviceImpl::sort_frontier)
-static __global__ void iota_kernel(uint32_t* p, uint64_t n) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    p[i] = (uint32_t)i;
-}
-static __global__ void unit_word_kernel(const uint32_t* units, uint32_t words, uint32_t off, const uint32_t* perm, uint64_t n,
-                                 uint32_t* keys) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    keys[i] = units[(uint64_t)perm[i] * words + off];
-}
-template <int WORDS>
-__global__ void gather_perm_kernel(const uint32_t* in, const uint32_t* perm, uint64_t n, uint32_t* out) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint4* s4 = (const uint4*)(in + (uint64_t)perm[i] * WORDS);
-    uint4* d4 = (uint4*)(out + i * WORDS);
-#pragma unroll
-    for (int q = 0; q < WORDS / 4; ++q) d4[q] = s4[q];
-  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -350,6 +331,16 @@ void launch_reduce(uint32_t mw, const uint32_t* records, uint64_t n, uint32_t ha
 void launch_min_best(unsigned long long* best64, uint32_t* poll_rep, unsigned long long v, hipStream_t s);
 void launch_gather_units(uint32_t words, const uint32_t* in, uint64_t offset, uint64_t stride, uint64_t cnt, uint32_t* out,
                          uint32_t blocks, hipStream_t s);
+// The frontier sort (radix passes over 32-bit keys with a permutation as values, hipCUB) and
+// its helpers: one instance, not one per engine shape (the sort's template instances were
+// ~2 MB of every part's code object).
+void sort_pairs_u32(void* temp, size_t* temp_bytes, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, int n,
+                    int end_bit, hipStream_t s);
+void launch_iota(uint32_t* p, uint64_t n, uint32_t blocks, hipStream_t s);
+void launch_unit_word(const uint32_t* units, uint32_t words, uint32_t off, const uint32_t* perm, uint64_t n, uint32_t* keys,
+                      uint32_t blocks, hipStream_t s);
+void launch_gather_perm(uint32_t words, const uint32_t* in, const uint32_t* perm, uint64_t n, uint32_t* out, uint32_t blocks,
+                        hipStream_t s);
 #if QI_PART <= 0
 namespace dev {
 // Fold a host-known best witness into the device-side one and its polled replicas (1-word keys).
@@ -421,6 +412,41 @@ void launch_gather_units(uint32_t words, const uint32_t* in, uint64_t offset, ui
   hipLaunchKernelGGL(dev::gather_units_kernel, dim3(blocks), dim3(256), 0, s, words, in, offset, stride, cnt, out);
 }
 #endif  // QI_PART <= 0
+#if QI_PART < 0 || QI_PART == 6  // the frontier sort: a code object of its own, loaded by the first sort
+namespace dev {
+static __global__ void iota_kernel(uint32_t* p, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = (uint32_t)i;
+}
+static __global__ void unit_word_kernel(const uint32_t* units, uint32_t words, uint32_t off, const uint32_t* perm, uint64_t n,
+                                        uint32_t* keys) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    keys[i] = units[(uint64_t)perm[i] * words + off];
+}
+static __global__ void gather_perm_kernel(uint32_t words, const uint32_t* in, const uint32_t* perm, uint64_t n, uint32_t* out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4* s4 = (const uint4*)(in + (uint64_t)perm[i] * words);
+    uint4* d4 = (uint4*)(out + i * words);
+    for (uint32_t q = 0; q < words / 4; ++q) d4[q] = s4[q];
+  }
+}
+}  // namespace dev
+void sort_pairs_u32(void* temp, size_t* temp_bytes, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, int n,
+                    int end_bit, hipStream_t s) {
+  HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, k_in, k_out, v_in, v_out, n, 0, end_bit, s));
+}
+void launch_iota(uint32_t* p, uint64_t n, uint32_t blocks, hipStream_t s) {
+  hipLaunchKernelGGL(dev::iota_kernel, dim3(blocks), dim3(256), 0, s, p, n);
+}
+void launch_unit_word(const uint32_t* units, uint32_t words, uint32_t off, const uint32_t* perm, uint64_t n, uint32_t* keys,
+                      uint32_t blocks, hipStream_t s) {
+  hipLaunchKernelGGL(dev::unit_word_kernel, dim3(blocks), dim3(256), 0, s, units, words, off, perm, n, keys);
+}
+void launch_gather_perm(uint32_t words, const uint32_t* in, const uint32_t* perm, uint64_t n, uint32_t* out, uint32_t blocks,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(dev::gather_perm_kernel, dim3(blocks), dim3(256), 0, s, words, in, perm, n, out);
+}
+#endif  // frontier sort
 
 // hipStreamCreate costs ~2.4 ms on this stack (measured, QI_TRACE; the first one of a process
 // far more): engines and the per-SCC checker take their stream from ONE per-device pool and
@@ -1418,24 +1444,20 @@ class SearchDeviceImpl : public SearchDevice {
         sp_[i] = dalloc<uint32_t>(sort_cap_);
       }
       stemp_bytes_ = 0;
-      HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, stemp_bytes_, sk_[0], sk_[1], sp_[0], sp_[1],
-                                                   (int)sort_cap_, 0, 32, stream_));
+      sort_pairs_u32(nullptr, &stemp_bytes_, sk_[0], sk_[1], sp_[0], sp_[1], (int)sort_cap_, 32, stream_);
       stemp_ = (void*)dalloc<uint8_t>(stemp_bytes_);
     }
     const uint32_t nb = (uint32_t)std::min<uint64_t>((n + 255) / 256, 65535);
-    hipLaunchKernelGGL(dev::iota_kernel, dim3(nb), dim3(256), 0, stream_, sp_[0], n);
+    launch_iota(sp_[0], n, nb, stream_);
     for (int pass = 0; pass <= MW; ++pass) {  // pass 0: depth; pass p: K[MW - p]
       const int off = pass == 0 ? UL::DEPTH : UL::K_ + MW - pass;
-      hipLaunchKernelGGL(dev::unit_word_kernel, dim3(nb), dim3(256), 0, stream_, units_[cur_], (uint32_t)UL::WORDS,
-                         (uint32_t)off, sp_[0], n, sk_[0]);
+      launch_unit_word(units_[cur_], (uint32_t)UL::WORDS, (uint32_t)off, sp_[0], n, sk_[0], nb, stream_);
       size_t tb = stemp_bytes_;
-      HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(stemp_, tb, sk_[0], sk_[1], sp_[0], sp_[1], (int)n, 0,
-                                                   pass == 0 ? 12 : 32, stream_));
+      sort_pairs_u32(stemp_, &tb, sk_[0], sk_[1], sp_[0], sp_[1], (int)n, pass == 0 ? 12 : 32, stream_);
       std::swap(sp_[0], sp_[1]);
     }
     ensure_cap(1 - cur_, n);
-    hipLaunchKernelGGL(dev::gather_perm_kernel<UL::WORDS>, dim3(nb), dim3(256), 0, stream_, units_[cur_], sp_[0], n,
-                       units_[1 - cur_]);
+    launch_gather_perm((uint32_t)UL::WORDS, units_[cur_], sp_[0], n, units_[1 - cur_], nb, stream_);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(stream_));
     cur_ = 1 - cur_;
@@ -1619,7 +1641,10 @@ template <int MW, int TW, int SMAX, bool ORD>
 std::unique_ptr<SearchDevice> make_engine(int device, const LocalFlat& f, const SearchConfig& cfg) {
   return std::unique_ptr<SearchDevice>(new SearchDeviceImpl<MW, TW, SMAX, ORD>(device, f, cfg));
 }
-#define QI_ENGINES_1(X) X(1, 1, 24, false) X(1, 2, 24, false) X(1, 4, 24, false) X(2, 2, 16, false) X(2, 4, 16, false)
+// (the one-word shape, the usual one for a real network's searched SCC, has a part -- a code
+// object -- of its own: the first run on a network loads only that, ~1 ms instead of 4-6)
+#define QI_ENGINES_5(X) X(1, 1, 24, false)
+#define QI_ENGINES_1(X) X(1, 2, 24, false) X(1, 4, 24, false) X(2, 2, 16, false) X(2, 4, 16, false)
 #define QI_ENGINES_2(X) X(4, 4, 12, false) X(4, 8, 12, false) X(8, 8, 8, false)
 #define QI_ENGINES_3(X) X(1, 1, 24, true) X(1, 4, 24, true) X(2, 4, 16, true) X(4, 8, 12, true)
 #define QI_ENGINES_4(X) X(8, 8, 8, true) X(16, 16, 8, true) X(32, 32, 8, true)
@@ -1632,6 +1657,7 @@ QI_ENGINES_1(QI_ENGINE_EXT)
 QI_ENGINES_2(QI_ENGINE_EXT)
 QI_ENGINES_3(QI_ENGINE_EXT)
 QI_ENGINES_4(QI_ENGINE_EXT)
+QI_ENGINES_5(QI_ENGINE_EXT)
 #elif QI_PART == 1
 QI_ENGINES_1(QI_ENGINE_DEF)
 #elif QI_PART == 2
@@ -1640,6 +1666,8 @@ QI_ENGINES_2(QI_ENGINE_DEF)
 QI_ENGINES_3(QI_ENGINE_DEF)
 #elif QI_PART == 4
 QI_ENGINES_4(QI_ENGINE_DEF)
+#elif QI_PART == 5
+QI_ENGINES_5(QI_ENGINE_DEF)
 #endif
 
 #if QI_PART <= 0
