@@ -1,12 +1,12 @@
 #!/usr/bin/env python
 """bench.py -- quorum-fixpoint evals/sec + time-to-verdict on a 256-validator tiered FBAS.
 
-Workload (BASELINE.json configs[3]): G2 two_tier(k_top, 256) -- a top tier
+Workload (BASELINE.json configs[3]): two_tier(k_top, 256) -- a top tier
 of k_top organisations x 3 validators (inner 2-of-3, outer ceil(2k/3)-of-k) that is the
 searched SCC, plus 256 - 3k lower validators in organisations of 3.  k_top = 10 by
 default: the repo's single-threaded -O3 CPU restatement of the reference needs 191.9 s for
 its full search on the GPU box's host (121,164,209 search nodes, 204,527,236 credited
-fixpoint evals; profiles/r02/cpu_full.json), inside the survey's 60-600 s window.
+fixpoint evals; profiles/r02/cpu_full.json), inside the 60-600 s window the workload was sized for.
 
 One "step" = one full solve of the resident FBAS: the per-SCC quorum checks (batched
 GFP kernel, cpp:649-672) plus the complete branch-and-bound search (cpp:348-400), i.e.
@@ -52,7 +52,7 @@ def ops_per_round(sh):
 
 
 def lds_bytes_per_round(sh):
-    """SURVEY.md §8d's LDS side: the bytes a Jacobi round would read if the threshold-node
+    """The roofline model's LDS side: the bytes a Jacobi round would read if the threshold-node
     masks sat in LDS (4 B per 32-bit word per vertex word and per child word, extra planes
     included).  The specialised kernel holds them as instruction literals / SGPRs instead,
     so this is the model's demand, not traffic the kernel issues."""
@@ -307,7 +307,7 @@ def main():
                           "(~35 T), the fixpoint's and+bcnt pair ~43 T (profiles/r02/peaks.json)"),
             "lds_model": {"bytes_per_launch": lds_launch, "achieved": lds_achieved, "peak": LDS_PEAK_TBS,
                           "unit": "TB/s", "frac": lds_achieved / LDS_PEAK_TBS,
-                          "note": "SURVEY §8d LDS-side model (TN masks per round); the kernel serves them from "
+                          "note": "LDS-side model (TN masks per round); the kernel serves them from "
                                   "instruction literals / SGPRs, so LDS is not the bound"},
             "kernel": "qi_search_spec (run-time specialised search_kernel)" if specialised else "search_kernel",
             "avg_launch_ms": avg_launch_ms,

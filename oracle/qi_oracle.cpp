@@ -13,7 +13,7 @@
 //    findBestNode          cpp:203-250    R5  (tie-break: "random" = reference reservoir
 //                                              sampling, "lowest" = lowest vertex index of
 //                                              the argmax set, one of the reference's
-//                                              possible outcomes -- SURVEY.md §8a-R5)
+//                                              possible outcomes, cpp:229-246)
 //    iterateMinimalQuorums cpp:252-346    R6  exclusion branch first, |D|>|scc|/2 prune
 //    checkMinimalQuorums   cpp:348-400    R4/R7 visitor with outside-SCC vertices available
 //    parseQuorumSet/JSON   cpp:402-436    boost::property_tree JSON semantics (values as text)

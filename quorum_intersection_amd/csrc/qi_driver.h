@@ -34,7 +34,7 @@ struct ShardConfig {
   uint64_t min_move = 64;
 };
 
-// One engine on `device` (the round-1 path).
+// One engine on `device`.
 SearchOutcome search_front_scc(const Graph& g, const std::vector<uint32_t>& scc, int device, const SearchConfig& cfg);
 
 // Sharded search: engine 0 grows the frontier from the root (cpp:393), every engine keeps

@@ -1,4 +1,4 @@
-"""Deterministic synthetic stellarbeat-format FBAS generators.
+"""Deterministic synthetic stellarbeat-format FBAS generators (benchmark and test workloads).
 
 The reference ships no generator; these produce JSON arrays in the exact input format
 parsed by quorum_intersection.cpp:420-436 (``publicKey``, ``name``, ``quorumSet`` with

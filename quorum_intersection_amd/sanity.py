@@ -1,7 +1,7 @@
 """Snapshot sanity filter: drop validators whose quorum set can never be satisfied.
 
 Host-side mirror of the reference's offline scrubber ``fix_quorum_configurations.py``
-(SURVEY.md §2 C17, §8(f) item 4), kept interface-compatible so that a pipeline of the form
+(fix_quorum_configurations.py:11-15), kept interface-compatible so that a pipeline of the form
 
     python fix_quorum_configurations.py < snapshot.json > fixed.json
 

@@ -38,7 +38,7 @@ def instances():
 
 
 def big_instances():
-    # BASELINE configs[2] ("64 orgs x 3 validators", SURVEY.md §8d: G2(k_top, 192))
+    # the "64 orgs x 3 validators" benchmark configuration: two_tier(k_top, 192)
     for k in (7, 8):
         yield f"two_tier_{k}_192", fbas_gen.two_tier(k, 192)
     for k in (9, 10):

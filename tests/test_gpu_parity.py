@@ -2,7 +2,7 @@
 
 Bar: bit-exact verdicts, preorder-exact search-node counts, exact credited fixpoint-eval
 counts, minimal quorums visited and witnesses, under the deterministic lowest-index
-tie-break (a possible execution of the reference's random one, SURVEY.md §8a-R5);
+tie-break (a possible execution of the reference's random one, cpp:229-246);
 bit-exact containsQuorum survivor sets.  Every test here runs HIP kernels on cuda:0.
 """
 import json
@@ -93,6 +93,25 @@ def test_gfp_batch_random(seed):
         assert sorted(g.contains_quorum(s, av)) == o
 
 
+def test_gfp_batch_large_batch_matches_small_batches():
+    # a batch up to 64 KB is read and written by the kernel straight in pinned host memory,
+    # a larger one goes through device buffers and two DMAs: same answers either way
+    text = random_org_fbas(11, 8, t0=False)
+    f, g = qa.FBAS(text), Oracle().load(text)
+    rng = random.Random(5)
+    base = random_masks(rng, f.n, 48, 0.7)
+    nodes = [base[i % len(base)] for i in range(6000)]           # 6000 x 3 x 8 B x words > 64 KB
+    nm = qa.masks_from_sets(nodes, f.n)
+    big = f.gfp_batch(nm, nm)
+    small = np.concatenate([f.gfp_batch(nm[i:i + 40], nm[i:i + 40]) for i in range(0, 240, 40)])
+    assert (big[:240] == small).all()
+    assert (big[:48] == big[48 * 124:48 * 125]).all()            # the same 48 queries, 124 rounds later
+    out = qa.sets_from_masks(big[:48], f.n)
+    for s, o in zip(base, out):
+        av = [v in set(s) for v in range(f.n)]
+        assert sorted(g.contains_quorum(s, av)) == o
+
+
 def test_contains_quorum_api_order():
     text = fixture_text("correct")
     f, g = qa.FBAS(text), Oracle().load(text)
@@ -151,7 +170,8 @@ def test_solve_two_tier_256():
 
 
 def test_tiered_8_full_search_counts():
-    # 1,857,737 search calls, 3,030,461 fixpoint evals, 20,412 minimal quorums
+    # an independent model of cpp:90-400 gave 1,857,737 search calls, 3,030,461 fixpoint evals,
+    # 20,412 minimal quorums
     for jit in (0, 1, 2):
         d = qa.FBAS(fbas_gen.tiered(8)).solve_stats(jit=jit)
         assert (d["verdict"], d["nodes"], d["evals"], d["minq"]) == (True, 1857737, 3030461 + 0, 20412)
@@ -199,7 +219,7 @@ def test_planted_deep_dealt(world, target, batch):
 def test_large_scc_multiword_masks(evict, monkeypatch):
     # |SCC| in (32, 64] and (64, 128]: 2- and 4-word masks (planted witnesses keep the
     # oracle's search short).  QI_EVICT = the eviction slots per lane reserved in the
-    # output buffer: round 1's rule "spill and stop after evict_max evictions" starved the
+    # output buffer: an earlier rule, "spill and stop after evict_max evictions", starved the
     # witness path at 8 (the frontier grew by 1.4 M units per launch, profiles/r02/
     # evict8_before.log); evictions now come from a shared pool and carried-over units go
     # first, so any reserve terminates.

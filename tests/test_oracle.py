@@ -49,8 +49,8 @@ def test_oracle_matches_golden(name):
         assert r[k] == v, (name, k)
 
 
-def test_survey_counts():
-    # SURVEY.md §6 (independent throwaway model at survey time)
+def test_independent_model_counts():
+    # counts from an independent throwaway model of cpp:90-400 written before the oracle
     o = Oracle()
     assert (o.load(fixture_text("correct")).solve()["nodes"], o.load(fixture_text("correct")).solve()["evals"]) == (11, 80)
     assert (o.load(fixture_text("broken")).solve()["nodes"], o.load(fixture_text("broken")).solve()["evals"]) == (7, 70)
@@ -58,7 +58,7 @@ def test_survey_counts():
     assert (r["nodes"], r["evals"], r["minq"]) == (111461, 220117, 1215)
 
 
-def test_broken_witness_is_the_survey_pair():
+def test_broken_witness_is_the_known_pair():
     g = Oracle().load(fixture_text("broken"))
     r = g.solve()
     ids = g.graph()["ids"]

@@ -7,6 +7,10 @@ set -o pipefail
 O=gpurun_out/r03f
 mkdir -p $O
 step() { echo "== $1" ; }
+# the complete CPU search (~190 s on one core) prints nothing: keep a heartbeat in gpurun_out/
+( while true; do sleep 45; date +%s >> $O/heartbeat.log; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 step tests && timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1 &&
 step smoke && timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
 step bench_cpu_full && timeout -k 10 600 python -u bench.py --steps 20 --warmup 2 --cpu-full > $O/bench_default.json 2> $O/bench_default.err &&
