@@ -867,6 +867,7 @@ class SearchDeviceImpl : public SearchDevice {
     totals_ = dalloc<unsigned long long>(16 * dev::TOT_SHARDS);
     best64_ = dalloc<unsigned long long>(1);
     poll_rep_ = dalloc<uint32_t>((size_t)dev::POLL_REPS * 32);
+    diag_waves_on_ = std::getenv("QI_DIAG_WAVES") != nullptr;  // diagnostics: per-wave timestamps of every launch
     HIP_CHECK(hipMemsetAsync(poll_rep_, 0xFF, (size_t)dev::POLL_REPS * 128, stream_));
     red_ = dalloc<unsigned long long>(4);
     keydev_ = dalloc<uint32_t>(dev::KEY_WORDS_MAX);
@@ -923,6 +924,7 @@ class SearchDeviceImpl : public SearchDevice {
     (void)hipFree(totals_);
     (void)hipFree(best64_);
     (void)hipFree(poll_rep_);
+    (void)hipFree(diag_waves_);
     (void)hipFree(red_);
     (void)hipFree(keydev_);
     (void)hipFree(wit_);
@@ -995,6 +997,10 @@ class SearchDeviceImpl : public SearchDevice {
       ensure_cap(1 - cur_, need);
       if (log_.empty() || log_.back().cap - log_.back().used < log_need(n_)) new_log_chunk(2 * log_need(n_));
     }
+    if (diag_waves_on_) {  // diagnostics: per-wave timestamps of every launch of this chain
+      if (!diag_waves_) diag_waves_ = dalloc<uint32_t>((size_t)kMaxBatch * blocks * 4);
+      HIP_CHECK(hipMemsetAsync(diag_waves_, 0, (size_t)kMaxBatch * blocks * 16, stream_));
+    }
     LogChunk& lc = log_.back();
     uint32_t seed[dev::CTR_WORDS] = {0};
     seed[dev::C_OUT] = (uint32_t)n_;
@@ -1017,6 +1023,7 @@ class SearchDeviceImpl : public SearchDevice {
     a.best64 = best64_;
     a.xbest = xbest_dev_ ? xbest_dev_ : best64_;
     a.poll_rep = poll_rep_;
+    a.diag_waves = nullptr;
     a.tiebreak = cfg_.tiebreak;
     a.tie_seed = cfg_.tie_seed;
     a.grow_budget = cfg_.grow_budget;
@@ -1050,6 +1057,7 @@ class SearchDeviceImpl : public SearchDevice {
       a.prev = ctr_ + (size_t)k * dev::CTR_WORDS;
       a.counters = ctr_ + (size_t)(k + 1) * dev::CTR_WORDS;
       a.host_ctr = hctr_dev_ + (size_t)k * dev::HC_WORDS;
+      if (diag_waves_) a.diag_waves = diag_waves_ + (size_t)k * blocks * 4;
       if (++seq_ == 0xFFFFFFFFu) seq_ = 1;  // (the replicas' reset value is never a sequence number)
       a.seq = seq_;
       if constexpr (ORD) {
@@ -1173,6 +1181,42 @@ class SearchDeviceImpl : public SearchDevice {
         diag_prev_[0] = c[dev::HC_DIAG];
         diag_prev_[1] = c[dev::HC_DIAG + 1];
         std::fprintf(stderr, "\n");
+      }
+    }
+    if (diag_waves_) {  // per launch: waves, and percentiles of wave life, start -> dry, dry -> end (us)
+      std::vector<uint32_t> dw((size_t)enq * blocks * 4);
+      HIP_CHECK(hipMemcpy(dw.data(), diag_waves_, dw.size() * 4, hipMemcpyDeviceToHost));
+      for (uint32_t j = 0; j < enq; ++j) {
+        std::vector<double> life, todry, tail, endt;
+        uint32_t t_first = 0xFFFFFFFFu;
+        for (uint32_t b = 0; b < blocks; ++b) {
+          const uint32_t* w = &dw[((size_t)j * blocks + b) * 4];
+          if (w[3]) t_first = std::min(t_first, w[0]);
+        }
+        for (uint32_t b = 0; b < blocks; ++b) {
+          const uint32_t* w = &dw[((size_t)j * blocks + b) * 4];
+          if (!w[3]) continue;
+          life.push_back((w[3] - w[0]) * 0.01);
+          endt.push_back((w[3] - t_first) * 0.01);
+          if (w[1]) {
+            todry.push_back((w[1] - w[0]) * 0.01);
+            tail.push_back((w[3] - w[1]) * 0.01);
+          }
+        }
+        if (life.empty()) continue;
+        auto pct = [](std::vector<double>& v, double p) {
+          if (v.empty()) return 0.0;
+          std::sort(v.begin(), v.end());
+          return v[std::min(v.size() - 1, (size_t)(p * (v.size() - 1) + 0.5))];
+        };
+        double sum = 0;
+        for (double x : life) sum += x;
+        std::fprintf(stderr,
+                     "[qi]     waves of launch %u: %zu, life avg %.1f p50 %.1f p90 %.1f max %.1f | end after launch start p10 %.1f "
+                     "p50 %.1f p90 %.1f max %.1f | start->dry p10 %.1f p50 %.1f p90 %.1f max %.1f | dry->end p50 %.1f p90 %.1f max %.1f us\n",
+                     j, life.size(), sum / life.size(), pct(life, .5), pct(life, .9), pct(life, 1), pct(endt, .1), pct(endt, .5),
+                     pct(endt, .9), pct(endt, 1), pct(todry, .1), pct(todry, .5), pct(todry, .9), pct(todry, 1), pct(tail, .5),
+                     pct(tail, .9), pct(tail, 1));
       }
     }
     if (!trace_) ms_sum = si.dispatch_ms;  // the chain's kernels back to back (<= 2 empty launches at its end)
@@ -1543,6 +1587,8 @@ class SearchDeviceImpl : public SearchDevice {
   unsigned long long* totals_ = nullptr;
   unsigned long long* best64_ = nullptr;
   uint32_t* poll_rep_ = nullptr;                    // [POLL_REPS][32]: polled best key + dry flag lines
+  uint32_t* diag_waves_ = nullptr;                  // QI_DIAG_WAVES: [launches of a chain][blocks][4] timestamps
+  bool diag_waves_on_ = false;
   uint32_t seq_ = 0;                                // launch sequence numbers
   uint64_t* xbest_host_ = nullptr;                  // the engines' shared best key (share_best)
   const unsigned long long* xbest_dev_ = nullptr;   // its device view

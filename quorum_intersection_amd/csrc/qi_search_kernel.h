@@ -399,6 +399,7 @@ struct SearchArgs {
                                  // word 2 the sequence number of the last launch seen dry.  Every
                                  // wave polling ONE best key / queue head serialised at that line
                                  // (~25 ns per access: 0.8 ms per search at 64-iteration polls).
+  uint32_t* diag_waves;          // QI_DIAG_WAVES builds: [blocks][4] start, dry, first spill, end (10 ns ticks)
   uint32_t seq;                  // this launch's sequence number (unique per engine, never 0xFFFFFFFF)
   uint32_t tiebreak;             // findBestNode ties: 0 lowest vertex index, 1 the seeded uniform draw
                                  // (informational: the rule is compiled into the kernel, search_body's TIE)
@@ -745,7 +746,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
   const uint64_t wave_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-#ifdef QI_DIAG_LAUNCH
+#if defined(QI_DIAG_LAUNCH) || defined(QI_DIAG_WAVES)
   const uint32_t diag_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
   uint32_t diag_dry = 0, diag_sp0 = 0, diag_spr = 0, diag_sp1 = 0, diag_loop0 = 0;  // 0 = did not happen
 #define QI_DIAG_MARK(v) do { if (!(v)) (v) = (uint32_t)__builtin_amdgcn_s_memrealtime() | 1u; } while (0)
@@ -1614,6 +1615,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #endif
   }
 
+#ifdef QI_DIAG_WAVES  // diagnostics without atomics: this wave's timestamps, one plain 16-byte store
+  if (lane == 0 && a.diag_waves) {
+    (void)diag_spr; (void)diag_sp1; (void)diag_loop0;
+    *(uint4*)(a.diag_waves + (size_t)blockIdx.x * 4) =
+        make_uint4(diag_t0, diag_dry, diag_sp0, (uint32_t)__builtin_amdgcn_s_memrealtime());
+  }
+#endif
 #ifdef QI_DIAG_LAUNCH
   if (lane == 0) {
     const uint32_t t1 = (uint32_t)__builtin_amdgcn_s_memrealtime();
