@@ -779,6 +779,7 @@ class SearchDeviceImpl : public SearchDevice {
     if (const char* e = std::getenv("QI_GROW")) cfg_.grow_budget = (uint32_t)std::max(1, std::atoi(e));
     if (const char* e = std::getenv("QI_EVICT")) cfg_.evict_max = (uint32_t)std::atoi(e);
     if (const char* e = std::getenv("QI_RUN_AT")) cfg_.run_at = (uint32_t)std::atoi(e);
+    if (const char* e = std::getenv("QI_LOOKAHEAD")) cfg_.lookahead = (uint32_t)std::max(1, std::atoi(e));
     if (const char* e = std::getenv("QI_MAX_FRONTIER_GB")) max_frontier_bytes_ = (uint64_t)std::atoll(e) << 30;
     jit_smax_ = ORD ? SMAX : jit_default_smax(MW, SMAX);
     if (ORD) cfg_.jit = 1;  // no run-time specialisation of the ordered kernel

@@ -606,6 +606,10 @@ constexpr int stamp_bucket(int f) {
 #endif
 // fast steps of a dry wave run with this many eligible lanes (no unit can be installed any
 // more, so waiting for a full iteration serves only quorum leaves and full stacks)
+// fast steps in growth launches too (their per-lane budget stays exact)
+#ifndef QI_GROW_FAST
+#define QI_GROW_FAST 1
+#endif
 #ifndef QI_FAST_MIN_DRY
 #define QI_FAST_MIN_DRY 8
 #endif
@@ -716,6 +720,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   uint32_t steps = 0;
   bool must_spill = false;  // an eviction found the pool empty: spill at the next iteration
   uint32_t limit = budget;  // per-lane step limit; shrinks to steps+grace when the queue dries
+  const bool exact_budget = budget <= 2u * (uint32_t)QI_FAST_STEPS;  // wave-uniform: a growth launch
   bool dry = false;         // wave-uniform: no unit left to claim (head >= n_in)
   // wave-uniform: the iteration at which a dry wave spills whatever its lanes still hold --
   // all lanes at once, so the wave reserves its output slots with ONE atomic
@@ -1068,13 +1073,16 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     // ---- (0) fast steps: pop or process one node per lane, common outcomes only --------
     // A lane whose node is a quorum leaf (cpp:281) or whose push would need an eviction is
     // held, uncommitted, for the full iteration; lanes without node and stack wait there too.
-    // (not in the growth launches: their per-lane node budget is the grow budget exactly)
-    if (budget > 2u * (uint32_t)QI_FAST_STEPS && best64 == ~0ull && !(MW > 1 && a.has_best)) {
+    if ((QI_GROW_FAST || !exact_budget) && best64 == ~0ull && !(MW > 1 && a.has_best)) {
       bool hold = false;
+      // (a growth launch's few lanes step while any of them can; its per-lane budget is exact,
+      // and `steps < limit` keeps it so.  Run launches let lanes overshoot a grace-period limit
+      // by a fast run: stopping them one by one would undo the wave's single spill)
+      const uint32_t fast_min = exact_budget ? 1u : (dry ? (uint32_t)QI_FAST_MIN_DRY : (uint32_t)QI_FAST_MIN);
 #pragma unroll 1
       for (int fs = 0; fs < QI_FAST_STEPS; ++fs) {
-        const bool elig = !done && !hold && (has || tvalid);
-        if ((uint32_t)__popcll(__ballot(elig)) < (dry ? (uint32_t)QI_FAST_MIN_DRY : (uint32_t)QI_FAST_MIN)) break;
+        const bool elig = !done && !hold && (has || tvalid) && (!exact_budget || steps < limit);
+        if ((uint32_t)__popcll(__ballot(elig)) < fast_min) break;
         ++wave_iters;
         ++iter;
 #ifdef QI_DIAG_FAST  // diagnostics: fast steps counted in the cooperative-phase counter
