@@ -515,7 +515,7 @@ constexpr int stamp_bucket(int f) {
     return f == F_POP ? 0 : f == F_INSTALL ? 1 : f == F_BEST ? 2 : f == F_PUSH ? 3 : f == F_FLUSH ? 4 : f == F_CLAIM ? 5 : -1;
   if (QI_STAMP_SET == 4)  // fast steps against everything else
     return f == F_FAST ? 0 : 1;
-  if (QI_STAMP_SET == 3)  // explicit waits only: unit loads at install, vmcnt drain at claim, LDS refill at pop
+  if (QI_STAMP_SET == 3)  // explicit waits only: unit loads at install, the queue head's atomic at claim, LDS refill at pop
     return f == F_W_INSTALL ? 0 : f == F_W_CLAIM ? 1 : f == F_W_POP ? 2 : -1;
   if (QI_STAMP_SET == 2)
     return f == F_FASTP ? 0 : f == F_FASTMIN ? 1 : f == F_COOP ? 2 : f == F_POLL ? 3 : f == F_SPILL ? 4
@@ -613,6 +613,10 @@ constexpr int stamp_bucket(int f) {
 #ifndef QI_FAST_MIN_DRY
 #define QI_FAST_MIN_DRY 8
 #endif
+// share of a full grid's input that is dealt out statically, as one slab per block (see static_end)
+#ifndef QI_SLAB_PCT
+#define QI_SLAB_PCT 75
+#endif
 // TIE: findBestNode's tie rule, fixed per kernel (a run-time choice in the node loop cost
 // 15-50 % per search): false = lowest vertex index, true = the seeded uniform draw.
 template <int MW, int TW, int SMAX, class EV, bool TIE = false>
@@ -659,7 +663,15 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
   const uint32_t n_in = pc[C_OUT];
   const uint32_t log_base = pc[C_LOGN];
   const uint32_t nb_used = min((n_in + (uint32_t)WAVE - 1u) / (uint32_t)WAVE, gridDim.x);
-  const uint32_t static_end = min(n_in, nb_used * (uint32_t)WAVE);
+  // Statically assigned units: block b owns the slab [b * slab, (b + 1) * slab), its lanes' first
+  // units and then pools of 64 taken without an atomic; only the rest of the input
+  // (QI_SLAB_PCT % of it is dealt out as slabs) is claimed dynamically, to even out the waves.
+  // The dynamic queue's head is ONE word: a full grid's waves run out of units in bursts,
+  // and each claim then waited ~3 us for that line (6.5 % of all wave cycles).
+  uint32_t slab = (uint32_t)WAVE;
+  if (nb_used == gridDim.x)
+    slab *= max(1u, (uint32_t)(((uint64_t)n_in * (uint32_t)QI_SLAB_PCT / 100u) / ((uint64_t)nb_used * WAVE)));
+  const uint32_t static_end = min(n_in, nb_used * slab);
   // evictions share what the final spills and the carried-over units leave of out_cap
   const uint64_t spill_need = (uint64_t)n_in + (uint64_t)nb_used * WAVE * spill_reserve(SMAX);
   const uint32_t evict_pool = spill_need < (uint64_t)a.out_cap ? (uint32_t)((uint64_t)a.out_cap - spill_need) : 0u;
@@ -796,12 +808,13 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     else return a.units_in[(size_t)fidx * UW + wi];
   };
   // the statically assigned first unit of this lane (no atomic)
-  if (blockIdx.x * WAVE + lane < n_in) {
-    fidx = blockIdx.x * WAVE + lane;
+  if (blockIdx.x * slab + lane < n_in) {
+    fidx = blockIdx.x * slab + lane;
     fpend = true;
     load_unit();
   }
-  uint32_t pool_next = 0, pool_end = 0;  // wave-uniform pool of claimed unit indices
+  // wave-uniform pool of claimed unit indices: the rest of this block's slab first
+  uint32_t pool_next = min(blockIdx.x * slab + (uint32_t)WAVE, n_in), pool_end = min((blockIdx.x + 1u) * slab, n_in);
   bool pool_dead = static_end >= n_in;
 
   // A closed segment's record is written at the end of the iteration (flush_record), not
@@ -990,8 +1003,14 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       if (pool_next >= pool_end) {
         if (pool_dead) break;
         uint32_t base = 0;
+#if defined(QI_STAMPS) && QI_STAMP_SET == 3  // the wait for the queue head (stamp set 3)
+        QI_STAMP(F_RESET);
+#endif
         if (lane == 0) base = static_end + atomicAdd(&cc[C_HEAD], (uint32_t)WAVE);
         base = lane0(base);
+#if defined(QI_STAMPS) && QI_STAMP_SET == 3
+        QI_STAMP(F_W_CLAIM);
+#endif
         if (base >= n_in) {
           pool_dead = true;
           // tell the waves that poll this line: no unit is left to claim in this launch
@@ -1004,7 +1023,6 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
       const uint32_t avail = pool_end - pool_next;
       const uint32_t r = rank_in(wm);
       if (want && r < avail) {
-        QI_WAIT_STAMP("vmcnt(0)", F_W_CLAIM);
         fidx = pool_next + r;
         fpend = true;
         want = false;

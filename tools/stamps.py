@@ -21,7 +21,7 @@ tot = sum(st)
 SETS = {0: ["pop+install", "poll", "spill", "fixpoints", "best+push+flush+claim", "leaf phases"],
         1: ["pop", "close+install", "dout/qd+best", "evict+push", "flush_record", "claim"],
         4: ["fast steps", "full iterations", "-", "-", "-", "-"],
-        3: ["install: vmcnt(0) wait", "claim: vmcnt(0) drain", "pop: LDS refill wait", "-", "-", "-"],
+        3: ["install: vmcnt(0) wait", "claim: wait for the queue head (atomic)", "pop: LDS refill wait", "-", "-", "-"],
         2: ["fastp (|D|<=qmin)", "fastmin (|D|=qmin+1)", "coop (|D|>=qmin+2)", "done+poll", "spill", "fixpoints"]}
 sset = 0
 for tok in os.environ.get("QI_JIT_DEFINES", "").split(","):
