@@ -858,10 +858,18 @@ class SearchDeviceImpl : public SearchDevice {
     ctr_ = dalloc<uint32_t>((size_t)(kMaxBatch + 1) * dev::CTR_WORDS);
     glob_ = dalloc<uint32_t>(2);
     HIP_CHECK(hipMemsetAsync(glob_, 0, 8, stream_));
-    HIP_CHECK(hipHostMalloc((void**)&hctr_, (size_t)kMaxBatch * dev::HC_WORDS * 4 + 64,
+    // pinned: the launches' published counters, the flag words of a chain's end, a snapshot of
+    // the running totals (copied with the flags at every chain end: reading the totals after
+    // a search then needs no device round trip) and the root unit
+    constexpr size_t kTotBytes = 16 * dev::TOT_SHARDS * sizeof(unsigned long long);
+    HIP_CHECK(hipHostMalloc((void**)&hctr_, (size_t)kMaxBatch * dev::HC_WORDS * 4 + 64 + kTotBytes + UL::BYTES,
                             hipHostMallocMapped | hipHostMallocCoherent));
     HIP_CHECK(hipHostGetDevicePointer((void**)&hctr_dev_, (void*)hctr_, 0));
     glob_host_ = hctr_ + (size_t)kMaxBatch * dev::HC_WORDS;
+    totals_host_ = (unsigned long long*)(hctr_ + (size_t)kMaxBatch * dev::HC_WORDS + 16);
+    root_host_ = (uint32_t*)(totals_host_ + 16 * dev::TOT_SHARDS);
+    std::memset((void*)totals_host_, 0, kTotBytes);
+    totals_host_valid_ = true;  // totals_ is zeroed below
     lap("counters+pinned");
     for (auto& e : ev_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDefault));
     lap("chain events");
@@ -944,15 +952,18 @@ class SearchDeviceImpl : public SearchDevice {
   void reset_root() override {
     DeviceGuard dg(device_);
     ensure_cap(0, 1);
-    std::vector<uint32_t> u(UL::WORDS, 0);
-    if constexpr (ORD) {  // toRemove = scc in ascending order, dontRemove = {} (cpp:393)
-      u[UL::TLEN] = m_;
-      for (uint32_t v = 0; v < m_; ++v) u[UL::TORD + v / UL::EPW] |= v << (32 / UL::EPW * (v % UL::EPW));
-    } else {
-      for (int w = 0; w < MW; ++w) u[UL::T_ + w] = scc_mask_[w];  // toRemove = scc, dontRemove = {} (cpp:393)
+    if (!root_ready_) {  // the root unit, kept in pinned memory: later resets only enqueue its copy
+      uint32_t* u = root_host_;
+      std::memset(u, 0, UL::BYTES);
+      if constexpr (ORD) {  // toRemove = scc in ascending order, dontRemove = {} (cpp:393)
+        u[UL::TLEN] = m_;
+        for (uint32_t v = 0; v < m_; ++v) u[UL::TORD + v / UL::EPW] |= v << (32 / UL::EPW * (v % UL::EPW));
+      } else {
+        for (int w = 0; w < MW; ++w) u[UL::T_ + w] = scc_mask_[w];  // toRemove = scc, dontRemove = {} (cpp:393)
+      }
+      root_ready_ = true;
     }
-    HIP_CHECK(hipMemcpyAsync(units_[cur_], u.data(), UL::BYTES, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    HIP_CHECK(hipMemcpyAsync(units_[cur_], root_host_, UL::BYTES, hipMemcpyHostToDevice, stream_));
     n_ = 1;
   }
 
@@ -974,6 +985,7 @@ class SearchDeviceImpl : public SearchDevice {
     StepInfo si;
     si.frontier_in = n_;
     if (n_ == 0) return si;
+    totals_host_valid_ = false;  // until this chain's end has copied the totals again
     // run-time specialised kernel: start compiling once the search proves non-trivial,
     // switch to it at the first step boundary after it is ready
     if (cfg_.jit == 0 && launches_ >= cfg_.jit_after && jit_state_.load() == 0 && jit_eligible(flat_)) start_jit();
@@ -1117,7 +1129,10 @@ class SearchDeviceImpl : public SearchDevice {
     }
     if (!trace_) HIP_CHECK(hipEventRecord(ev_[1], stream_));  // the whole chain, first launch to last
     HIP_CHECK(hipMemcpyAsync((void*)glob_host_, glob_, 8, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync((void*)totals_host_, totals_, 16 * dev::TOT_SHARDS * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
+    totals_host_valid_ = true;
     for (; folded < enq; ++folded) fold_best(folded);
     const uint32_t g_wit = glob_host_[0], g_flags = glob_host_[1];
     if (g_flags & dev::FLAG_OUT_OVERFLOW) throw Error(QI_ERR_CAPACITY, "search frontier buffer overflow");
@@ -1418,10 +1433,14 @@ class SearchDeviceImpl : public SearchDevice {
   }
 
   Totals running_totals() const override {
-    DeviceGuard dg(device_);
     std::vector<unsigned long long> sh(16 * dev::TOT_SHARDS);
-    HIP_CHECK(hipMemcpyAsync(sh.data(), totals_, sh.size() * 8, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    if (totals_host_valid_) {  // nothing ran since the last chain end (or the last reset)
+      std::memcpy(sh.data(), (const void*)totals_host_, sh.size() * 8);
+    } else {
+      DeviceGuard dg(device_);
+      HIP_CHECK(hipMemcpyAsync(sh.data(), totals_, sh.size() * 8, hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
     unsigned long long r[16] = {0};
     for (int q = 0; q < dev::TOT_SHARDS; ++q)
       for (int i = 0; i < 16; ++i) r[i] += sh[(size_t)q * 16 + i];
@@ -1442,6 +1461,8 @@ class SearchDeviceImpl : public SearchDevice {
     for (auto& c : log_) c.used = 0;
     DeviceGuard dg(device_);
     HIP_CHECK(hipMemsetAsync(totals_, 0, 16 * dev::TOT_SHARDS * sizeof(unsigned long long), stream_));
+    std::memset((void*)totals_host_, 0, 16 * dev::TOT_SHARDS * sizeof(unsigned long long));
+    totals_host_valid_ = true;
     // no-witness best key; stream-ordered before every later launch, no host round trip
     HIP_CHECK(hipMemsetAsync(best64_, 0xFF, 8, stream_));
     HIP_CHECK(hipMemsetAsync(poll_rep_, 0xFF, (size_t)dev::POLL_REPS * 128, stream_));
@@ -1586,6 +1607,10 @@ class SearchDeviceImpl : public SearchDevice {
   hipEvent_t ev_[kMaxBatch + 1] = {};
   uint64_t stops_ = 0;
   unsigned long long* totals_ = nullptr;
+  unsigned long long* totals_host_ = nullptr;  // pinned snapshot of totals_ (valid: see running_totals)
+  bool totals_host_valid_ = false;
+  uint32_t* root_host_ = nullptr;              // pinned root unit
+  bool root_ready_ = false;
   unsigned long long* best64_ = nullptr;
   uint32_t* poll_rep_ = nullptr;                    // [POLL_REPS][32]: polled best key + dry flag lines
   uint32_t* diag_waves_ = nullptr;                  // QI_DIAG_WAVES: [launches of a chain][blocks][4] timestamps

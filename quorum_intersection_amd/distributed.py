@@ -343,8 +343,8 @@ def _gather_state(be: SearchBackend, device, group) -> Tuple[List[int], List[Opt
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t, group=group)
     sizes, keys = [], []
-    for o in out:
-        v = [int(x) for x in o.tolist()]
+    for v in torch.stack(out).tolist():  # one device-to-host copy for all ranks' rows
+        v = [int(x) for x in v]
         sizes.append(v[0])
         keys.append((tuple(v[3:3 + kw]), v[2]) if v[1] else None)
     return sizes, keys
@@ -439,9 +439,8 @@ def distributed_search(be: SearchBackend, group=None, device="cpu", lanes: int =
                     _settle(buf)
                     be.import_(cnt, buf)
                 moved += cnt
-    # (4) preorder-exact totals against the global best witness
-    sizes, keys = _gather_state(be, device, group) if world > 1 else ([0], [be.local_best()])
-    best = best_of(keys)
+    # (4) preorder-exact totals against the global best witness: the loop's last exchange
+    # (every frontier empty, no launch since) already holds every rank's final best key
     loc = be.reduce(best)
     tot = [int(loc["nodes"]), int(loc["evals"]), int(loc["minq"]), int(loc["zero_fallback"]), int(loc["rounds"]),
            launches, int(loc.get("units", 0)), int(loc.get("wave_iters", 0)), int(loc.get("coop_phases", 0))]
