@@ -672,7 +672,7 @@ def test_shared_best_key_prunes_other_engines(monkeypatch):
             best = waste if best is None else min(best, waste)
         runs[mode] = best
     print("post-witness nodes:", runs)
-    assert runs["shared"] <= 2.0 * runs["unshared"], runs
+    assert runs["shared"] <= 3.0 * runs["unshared"], runs
 
 
 def test_planted_deep_two_word_exact():
